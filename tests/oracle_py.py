@@ -1,0 +1,192 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module; the
+product path (nobs-whisper_amd/) never imports or links it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+class OracleParams(C.Structure):
+    _fields_ = [
+        ("language", C.c_char_p), ("initial_prompt", C.c_char_p),
+        ("n_max_text_ctx", C.c_int), ("offset_ms", C.c_int), ("duration_ms", C.c_int),
+        ("translate", C.c_int), ("no_context", C.c_int), ("no_timestamps", C.c_int),
+        ("single_segment", C.c_int), ("print_special", C.c_int), ("suppress_blank", C.c_int),
+        ("max_tokens", C.c_int),
+        ("temperature", C.c_float), ("temperature_inc", C.c_float), ("max_initial_ts", C.c_float),
+        ("length_penalty", C.c_float), ("entropy_thold", C.c_float), ("logprob_thold", C.c_float),
+        ("no_speech_thold", C.c_float),
+        ("best_of", C.c_int), ("fixed_tokens", C.c_int),
+    ]
+
+
+def reference_params(language: str | None = "en", prompt: str | None = None, fixed_tokens: int = 0) -> OracleParams:
+    """whisper_full_default_params(GREEDY) + the setters of src-tauri/src/whisper.rs:88-124."""
+    p = OracleParams()
+    p.language = language.encode() if language else None
+    p.initial_prompt = prompt.encode() if prompt else None
+    p.n_max_text_ctx = 16384
+    p.offset_ms = p.duration_ms = 0
+    p.translate = 0; p.no_context = 0; p.no_timestamps = 0; p.single_segment = 0
+    p.print_special = 0; p.suppress_blank = 1; p.max_tokens = 0
+    p.temperature = 0.0; p.temperature_inc = 0.2; p.max_initial_ts = 1.0; p.length_penalty = -1.0
+    p.entropy_thold = 2.4; p.logprob_thold = -1.0; p.no_speech_thold = 0.6
+    p.best_of = 1
+    p.fixed_tokens = fixed_tokens
+    return p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp, ip, fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_float)
+        sig = {
+            "oracle_load": (vp, [C.c_char_p, C.c_int, C.c_int]),
+            "oracle_free": (None, [vp]),
+            "oracle_set_threads": (None, [vp, C.c_int]),
+            "oracle_state_new": (vp, [vp]),
+            "oracle_state_free": (None, [vp]),
+            "oracle_token": (C.c_int, [vp, C.c_char_p]),
+            "oracle_mel": (C.c_int, [vp, vp, fp, C.c_int, ip]),
+            "oracle_state_mel": (None, [vp, fp]),
+            "oracle_set_mel": (None, [vp, vp, fp, C.c_int]),
+            "oracle_encode": (None, [vp, vp, C.c_int, fp]),
+            "oracle_cross_kv": (None, [vp, vp, C.c_int, fp, fp]),
+            "oracle_kv_clear": (None, [vp]),
+            "oracle_decode": (None, [vp, vp, ip, C.c_int, C.c_int, fp]),
+            "oracle_tokenize": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
+            "oracle_token_str": (C.c_char_p, [vp, C.c_int]),
+            "oracle_lang_detect": (C.c_int, [vp, vp]),
+            "oracle_full": (C.c_int, [vp, vp, C.POINTER(OracleParams), fp, C.c_int]),
+            "oracle_n_segments": (C.c_int, [vp]),
+            "oracle_segment_text": (C.c_char_p, [vp, C.c_int]),
+            "oracle_segment_t": (None, [vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+            "oracle_segment_n_tokens": (C.c_int, [vp, C.c_int]),
+            "oracle_segment_token": (C.c_int, [vp, C.c_int, C.c_int]),
+            "oracle_lang": (C.c_int, [vp]),
+            "oracle_no_speech": (C.c_float, [vp]),
+            "oracle_n_steps": (C.c_int, [vp]),
+            "oracle_step_margins": (None, [vp, fp]),
+            "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
+            "oracle_mel_tables": (None, [fp, fp, fp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+class Oracle:
+    """One loaded model + one state (mirrors whisper_context + whisper_state)."""
+
+    def __init__(self, path: str, mode: int = 1, n_threads: int = 8):
+        self.L = lib()
+        self.m = self.L.oracle_load(path.encode(), mode, n_threads)
+        if not self.m:
+            raise RuntimeError(f"oracle failed to load {path}")
+        self.s = self.L.oracle_state_new(self.m)
+        import struct
+        with open(path, "rb") as f:
+            f.read(4)
+            hp = struct.unpack("<11i", f.read(44))
+        (self.n_vocab, self.n_audio_ctx, self.d, self.n_head, self.n_enc, self.n_text_ctx, _, _,
+         self.n_dec, self.n_mels, _) = hp
+
+    def close(self):
+        if self.m:
+            self.L.oracle_state_free(self.s)
+            self.L.oracle_free(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def token(self, which: str) -> int:
+        return self.L.oracle_token(self.m, which.encode())
+
+    def mel(self, pcm: np.ndarray):
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        org = C.c_int()
+        n_len = self.L.oracle_mel(self.m, self.s, _fp(pcm), len(pcm), C.byref(org))
+        out = np.empty((self.n_mels, n_len), np.float32)
+        self.L.oracle_state_mel(self.s, _fp(out))
+        return out, org.value
+
+    def set_mel(self, mel: np.ndarray):
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        self.L.oracle_set_mel(self.m, self.s, _fp(mel), mel.shape[1])
+
+    def encode(self, seek: int = 0) -> np.ndarray:
+        out = np.empty((self.n_audio_ctx, self.d), np.float32)
+        self.L.oracle_encode(self.m, self.s, seek, _fp(out))
+        return out
+
+    def cross_kv(self, layer: int):
+        k = np.empty((self.n_audio_ctx, self.d), np.float32)
+        v = np.empty_like(k)
+        self.L.oracle_cross_kv(self.m, self.s, layer, _fp(k), _fp(v))
+        return k, v
+
+    def kv_clear(self):
+        self.L.oracle_kv_clear(self.s)
+
+    def decode(self, tokens, n_past: int) -> np.ndarray:
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.empty((len(t), self.n_vocab), np.float32)
+        self.L.oracle_decode(self.m, self.s, _ip(t), len(t), n_past, _fp(out))
+        return out
+
+    def tokenize(self, text: str):
+        buf = np.empty(4096, np.int32)
+        n = self.L.oracle_tokenize(self.m, text.encode(), _ip(buf), len(buf))
+        return buf[:n].tolist()
+
+    def token_str(self, i: int) -> bytes:
+        return self.L.oracle_token_str(self.m, i)
+
+    def full(self, pcm: np.ndarray, params: OracleParams) -> dict:
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        rc = self.L.oracle_full(self.m, self.s, C.byref(params), _fp(pcm), len(pcm))
+        segs = []
+        for i in range(self.L.oracle_n_segments(self.s)):
+            t0, t1 = C.c_int64(), C.c_int64()
+            self.L.oracle_segment_t(self.s, i, C.byref(t0), C.byref(t1))
+            toks = [self.L.oracle_segment_token(self.s, i, j) for j in range(self.L.oracle_segment_n_tokens(self.s, i))]
+            segs.append(dict(t0=t0.value, t1=t1.value, text=self.L.oracle_segment_text(self.s, i), tokens=toks))
+        n = self.L.oracle_n_steps(self.s)
+        margins = np.empty(n, np.float32)
+        self.L.oracle_step_margins(self.s, _fp(margins))
+        return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
+                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins)
