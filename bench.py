@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: audio-seconds/s of greedy Whisper transcription on MI355X.
+
+Metric (BASELINE.json): "audio-sec/s (RTF^-1) large-v3 greedy, batch 128; 1/2/4/8 MI355X".
+One step = whisper_mi355x_full_batch over this rank's batch of 30 s chunks (PCM already resident
+in HBM): log-mel -> encoder -> cross-KV -> prefill -> fixed-work greedy decode of --tokens tokens
+per chunk (EOT suppressed, no fallback: SURVEY.md §8d's reproducible-work mode for random
+weights) -> logits processing -> segments. Weak scaling: every rank processes --batch chunks;
+ranks shard chunks with no data-path collective; weights are loaded by rank 0 and broadcast once
+over RCCL/xGMI (outside the timed region).
+
+Model weights are a seeded synthetic GGML file of the named architecture (no checkpoints
+offline); audio is synthetic (tools/make_model.synthetic_pcm, seed 1234+chunk index).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "audio-sec/s (RTF⁻¹) large-v3 greedy, batch 128; 1/2/4/8 MI355X"
+K_NAMES = ["gemm_encoder", "attn_encoder", "attn_cross_decode", "attn_self_decode", "gemm_decode", "logits", "mel"]
+K_BOUND = ["mfma", "mfma", "hbm", "hbm", "hbm", "hbm", "hbm"]
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFS = 2500.0       # dense bf16/f16 MFMA peak (no sparsity)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_wrs():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("whisper_rs", os.path.join(ROOT, "nobs-whisper_amd", "whisper_rs.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def ensure_model(path: str, shape: str):
+    from make_model import write_model
+    if not os.path.exists(path):
+        t = time.time()
+        write_model(path, shape, 0)
+        log(f"[bench] wrote synthetic {shape} model to {path} in {time.time() - t:.1f}s")
+
+
+def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: int = 8) -> dict:
+    """The CPU oracle (restated whisper.cpp algorithm, C++/OpenMP) on a bounded sample of the same
+    workload: 1 chunk = mel + encoder + cross-KV + 3-token prefill + n_sample_tokens decode steps,
+    extrapolated to n_tokens decode steps per chunk."""
+    from make_model import synthetic_pcm
+    from oracle_py import Oracle
+    o = Oracle(model_path, mode=1, n_threads=threads)
+    pcm = synthetic_pcm(0)
+    t0 = time.time()
+    o.mel(pcm)
+    t1 = time.time()
+    o.encode(0)
+    t2 = time.time()
+    o.kv_clear()
+    sot = o.token("sot")
+    prompt = [sot, sot + 1, o.token("transcribe")]
+    lg = o.decode(prompt, 0)
+    t3 = time.time()
+    tok = int(lg[-1].argmax())
+    for i in range(n_sample_tokens):
+        lg = o.decode([tok], len(prompt) + i)
+        tok = int(lg[-1].argmax())
+    t4 = time.time()
+    o.close()
+    per_step = (t4 - t3) / n_sample_tokens
+    chunk_s = (t1 - t0) + (t2 - t1) + (t3 - t2) + n_tokens * per_step
+    return dict(value=30.0 / chunk_s, unit="audio-sec/s", cores=threads, kind="port",
+                sample=(f"1 x 30 s chunk: mel {t1 - t0:.2f}s + encoder/cross-KV {t2 - t1:.2f}s + prefill {t3 - t2:.2f}s "
+                        f"+ {n_sample_tokens} decode steps ({per_step * 1e3:.0f} ms/step) measured, extrapolated to "
+                        f"{n_tokens} steps/chunk; oracle/ = restated whisper.cpp CPU algorithm (not whisper.cpp), "
+                        f"{threads} OpenMP threads"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--batch", type=int, default=128, help="30 s chunks per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--tokens", type=int, default=128, help="decode tokens per chunk (fixed-work mode)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--model-dir", default=os.environ.get("NW_MODEL_DIR", "/tmp/nw_models"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    wrs = load_wrs()
+    os.makedirs(args.model_dir, exist_ok=True)
+    model_path = os.path.join(args.model_dir, f"{args.model}_s0.bin")
+    if local_rank == 0:
+        ensure_model(model_path, args.model)
+    barrier()
+
+    # ---- context: rank 0 loads, the others receive the weight arena over RCCL (xGMI) -------------
+    dtype = wrs.BF16 if args.dtype == "bf16" else wrs.F16
+    t_load = time.time()
+    ctx = wrs.WhisperContext(model_path, dtype=dtype, gpu_device=local_rank, load_weights=(rank == 0 or world == 1))
+    load_s = time.time() - t_load
+    bcast_s = 0.0
+    if world > 1:
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            assert wrs.lib().whisper_mi355x_rccl_unique_id(uid) == 0
+        obj = [bytes(uid.raw)]
+        dist.broadcast_object_list(obj, src=0)
+        t = time.time()
+        rc = wrs.lib().whisper_mi355x_broadcast_weights(ctx.ptr, obj[0], rank, world)
+        assert rc == 0, rc
+        bcast_s = time.time() - t
+    st = ctx.create_state()
+
+    # ---- this rank's chunks, resident in HBM --------------------------------------------------------
+    from make_model import synthetic_pcm
+    L = wrs.lib()
+    n = 16000 * 30
+    buf = L.whisper_mi355x_dev_alloc(ctx.ptr, args.batch * n * 4)
+    assert buf
+    host = np.empty(n, np.float32)
+    for i in range(args.batch):
+        host[:] = synthetic_pcm(rank * args.batch + i)
+        L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(buf + i * n * 4), host.ctypes.data, n * 4, 1)
+    jobs = [(buf + i * n * 4, n) for i in range(args.batch)]
+    params = wrs.reference_full_params("en")
+
+    def step():
+        rc = st.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
+        assert rc == 0, rc
+
+    # warmup (untimed) with every kernel class timed once to find the dominant kernel
+    L.whisper_mi355x_kernel_timing(st.ptr, 0x7F)
+    tw = time.time()
+    for _ in range(args.warmup):
+        step()
+    warm_s = (time.time() - tw) / max(1, args.warmup)
+    stats = []
+    for k in range(len(K_NAMES)):
+        out = (C.c_double * 3)()
+        L.whisper_mi355x_kernel_stats(st.ptr, k, out)
+        stats.append(tuple(out))
+    dom = max(range(len(K_NAMES)), key=lambda k: stats[k][0])
+    share = {K_NAMES[k]: round(stats[k][0] / max(1e-9, sum(s[0] for s in stats)), 4) for k in range(len(K_NAMES))}
+
+    # timed region: only the dominant class is event-timed (keeps event overhead off the others)
+    L.whisper_mi355x_kernel_timing(st.ptr, 1 << dom)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.time() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    out = (C.c_double * 3)()
+    L.whisper_mi355x_kernel_stats(st.ptr, dom, out)
+    k_ms, k_cnt, k_work = out[0], out[1], out[2]
+    phases = st.phase_ms()
+    decoded = L.whisper_mi355x_batch_decoded_tokens(st.ptr)
+
+    if rank == 0:
+        audio_s = 30.0 * args.batch * world * args.steps
+        value = audio_s / elapsed
+        if K_BOUND[dom] == "mfma":
+            achieved = k_work / (k_ms * 1e-3) / 1e12
+            roof = dict(bound="mfma", achieved=round(achieved, 2), peak=MFMA_PEAK_TFS, unit="TFLOP/s",
+                        frac=round(achieved / MFMA_PEAK_TFS, 4), traffic=None)
+        else:
+            achieved = k_work / (k_ms * 1e-3) / 1e9
+            roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
+        roof.update(kernel=K_NAMES[dom], launches=int(k_cnt), avg_launch_ms=round(k_ms / max(1, k_cnt), 4),
+                    work_per_launch=k_work / max(1, k_cnt), time_share_warmup=share)
+        cpu = None
+        if args.cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(model_path, args.cpu_threads, args.tokens)
+            except Exception as e:  # reported, never fatal to the GPU number
+                cpu = dict(value=None, unit="audio-sec/s", cores=args.cpu_threads, kind="port", sample=f"failed: {e}")
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "audio-sec/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (seeded AM-harmonic 30 s PCM; seeded random weights of the named architecture)",
+            "config": {"workload": f"{args.model} {args.dtype} greedy, {args.batch} x 30 s chunks per GPU, "
+                                   f"fixed {args.tokens}-token decode per chunk, language en, no prompt",
+                       "model": args.model, "global_batch": args.batch * world, "batch_per_gpu": args.batch,
+                       "tokens_per_chunk": args.tokens, "seq_len": 1500,
+                       "parallelism": f"dp{world} (chunk sharding, RCCL weight broadcast only)"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "extra": {"rtf_inverse_per_gpu": round(value / world, 2), "decoded_tokens_per_step": decoded,
+                      "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
+                      "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),
+                      "weight_broadcast_s": round(bcast_s, 3)},
+        }
+        print(json.dumps(line), flush=True)
+    L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(buf))
+    st.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+/*
+ * whisper_mi355x.h — additive extensions of the whisper.h ABI for MI355X (SURVEY.md §8b
+ * "Additive batch extension"). The reference calls one clip at a time
+ * (src-tauri/src/whisper.rs:150-151: "GPU can only process one at a time"); these entry points
+ * let a caller hand over many independent 30 s chunks at once, keep PCM resident in HBM, pick
+ * the compute type, and broadcast weights to the other GPUs of a node over RCCL/xGMI.
+ * Nothing here replaces a reference interface; whisper.h's functions are unchanged.
+ */
+#ifndef WHISPER_MI355X_H
+#define WHISPER_MI355X_H
+
+#include "whisper.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* compute type of weights and GEMM activations */
+enum whisper_mi355x_dtype { WHISPER_MI355X_F16 = 0, WHISPER_MI355X_BF16 = 1 };
+
+/* Context on HIP device `gpu_device` (from params) with an explicit compute type.
+ * load_weights = false: parse the file and allocate the device weight arena without filling it
+ * (a rank that receives the weights by whisper_mi355x_broadcast_weights). */
+WHISPER_API struct whisper_context * whisper_mi355x_init(const char * path_model, struct whisper_context_params params,
+                                                         int dtype, bool load_weights);
+
+/* Device weight arena (one contiguous allocation holding every converted tensor). */
+WHISPER_API int whisper_mi355x_weight_arena(struct whisper_context * ctx, void ** dev_ptr, size_t * bytes);
+
+/* RCCL (rccl.h) unique id for a weight broadcast: filled by rank 0, shipped to the other ranks by
+ * the caller (any side channel), then every rank calls whisper_mi355x_broadcast_weights. */
+WHISPER_API int whisper_mi355x_rccl_unique_id(char out[128]);
+WHISPER_API int whisper_mi355x_broadcast_weights(struct whisper_context * ctx, const char unique_id[128], int rank, int world);
+
+/* Batched whisper_full: n_jobs independent clips, each processed exactly as one
+ * whisper_full_with_state call on a fresh state would process it. pcm[j] points at n_samples[j]
+ * f32 samples, on the host (pcm_on_device = false) or already in this context's HBM (true).
+ * Fixed-work benchmark mode: fixed_tokens > 0 decodes exactly that many tokens per window with EOT
+ * suppressed and no temperature fallback. Returns 0 on success. */
+WHISPER_API int whisper_mi355x_full_batch(struct whisper_context * ctx, struct whisper_state * state,
+                                          struct whisper_full_params params, const float * const * pcm,
+                                          const int * n_samples, int n_jobs, bool pcm_on_device, int fixed_tokens);
+WHISPER_API int whisper_mi355x_batch_n_segments(struct whisper_state * state, int job);
+WHISPER_API const char * whisper_mi355x_batch_segment_text(struct whisper_state * state, int job, int i_segment);
+WHISPER_API int64_t whisper_mi355x_batch_segment_t0(struct whisper_state * state, int job, int i_segment);
+WHISPER_API int64_t whisper_mi355x_batch_segment_t1(struct whisper_state * state, int job, int i_segment);
+WHISPER_API int whisper_mi355x_batch_segment_n_tokens(struct whisper_state * state, int job, int i_segment);
+WHISPER_API whisper_token_data whisper_mi355x_batch_token_data(struct whisper_state * state, int job, int i_segment, int i_token);
+WHISPER_API int whisper_mi355x_batch_lang_id(struct whisper_state * state, int job);
+/* tokens generated (all decode steps, all attempts) by the last whisper_mi355x_full_batch */
+WHISPER_API long whisper_mi355x_batch_decoded_tokens(struct whisper_state * state);
+
+/* Phase timings of the last full/full_batch call, milliseconds (host wall clock around
+ * stream-synchronised phases): mel, encode (incl. cross-KV), prefill, decode steps, logits. */
+WHISPER_API int whisper_mi355x_phase_ms(struct whisper_state * state, double out[5]);
+
+/* Normalised log-mel of the last whisper_pcm_to_mel_with_state / whisper_full_with_state call,
+ * copied to host: [n_mel][n_len] f32. Returns n_len. */
+WHISPER_API int whisper_mi355x_get_mel(struct whisper_state * state, float * out, int cap_floats);
+/* Encoder output (ln_post) of window 0 of the last encode, [n_audio_ctx][n_audio_state] f32. */
+WHISPER_API int whisper_mi355x_get_encoder_out(struct whisper_state * state, float * out, int cap_floats);
+
+/* Live per-kernel-class timing with HIP events on the state's stream (used by bench.py for the
+ * roofline). Classes: 0 encoder-side GEMM (work = FLOPs), 1 encoder attention (FLOPs),
+ * 2 decoder cross-attention (HBM bytes), 3 decoder self-attention (bytes), 4 decoder GEMM (bytes),
+ * 5 logits processing (bytes), 6 mel (bytes). class_mask bit k times class k (0 = off); every call
+ * resets the counters; stats out =
+ * {total ms, launches, total work}. */
+WHISPER_API int whisper_mi355x_kernel_timing(struct whisper_state * state, int class_mask);
+WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cls, double out[3]);
+
+/* ABI self-description, no device needed: sizeof(whisper_full_params), sizeof(whisper_context_params),
+ * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /
+ * new_segment_callback / vad_params). Lets a binding (bindgen, ctypes) be checked field-by-field. */
+WHISPER_API int whisper_mi355x_abi_layout(size_t out[8]);
+
+/* HIP stream of a state (hipStream_t), for callers that enqueue their own work around it. */
+WHISPER_API void * whisper_mi355x_state_stream(struct whisper_state * state);
+
+/* Model-free micro-API used by the kernel parity tests: allocate/copy device memory on the
+ * context's device. */
+WHISPER_API void * whisper_mi355x_dev_alloc(struct whisper_context * ctx, size_t bytes);
+WHISPER_API void   whisper_mi355x_dev_free(struct whisper_context * ctx, void * p);
+WHISPER_API int    whisper_mi355x_memcpy(struct whisper_context * ctx, void * dst, const void * src, size_t bytes, int kind);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WHISPER_MI355X_H */

@@ -1,0 +1,85 @@
+// Shared definitions for the MI355X (gfx950) Whisper engine: error handling, element types,
+// vector types for 16-byte loads and MFMA fragments.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define WM_CHECK(x)                                                                              \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) {                                                                  \
+            fprintf(stderr, "whisper_mi355x: HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), \
+                    __FILE__, __LINE__, #x);                                                     \
+            abort();                                                                             \
+        }                                                                                        \
+    } while (0)
+
+namespace wm {
+
+// Compute element type of the weights and the GEMM-side activations.
+//  F16  — the GGML file's own weight type; reproduces ggml's f16 roundings (parity mode).
+//  BF16 — weights rounded f16->bf16 at load; same MFMA rate, wider exponent.
+enum class DType : int { F16 = 0, BF16 = 1 };
+
+typedef _Float16 half_t;
+typedef __bf16 bf16_t;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct Frag;
+template <> struct Frag<half_t> { typedef half8 type; };
+template <> struct Frag<bf16_t> { typedef bfx8 type; };
+
+__device__ __forceinline__ f32x4 mfma16x16x32(half8 a, half8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x16x32(bfx8 a, bfx8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T> __device__ __forceinline__ T to_t(float x) { return (T)x; }
+template <typename T> __device__ __forceinline__ float from_t(T x) { return (float)x; }
+
+// whisper.cpp/ggml GELU (GGML_GELU_FP16 path): f16(x) -> f16(gelu_tanh(x)); |x|>=10 shortcuts.
+__device__ __forceinline__ float gelu_ggml(float x) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    const float h = (float)(half_t)x;
+    const float GELU_COEF_A = 0.044715f;
+    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    const float g = 0.5f * h * (1.0f + tanhf(SQRT_2_OVER_PI * h * (1.0f + GELU_COEF_A * h * h)));
+    return (float)(half_t)g;
+}
+
+// host-side conversions (weights are converted once at load)
+static inline float h2f(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t exp = (h >> 10) & 0x1f, mant = h & 0x3ffu, x;
+    if (exp == 0) {
+        if (mant == 0) x = sign;
+        else {
+            int e = -1;
+            do { e++; mant <<= 1; } while (!(mant & 0x400u));
+            mant &= 0x3ffu;
+            x = sign | ((uint32_t)(127 - 15 - e) << 23) | (mant << 13);
+        }
+    } else if (exp == 0x1f) x = sign | 0x7f800000u | (mant << 13);
+    else x = sign | ((exp + 127 - 15) << 23) | (mant << 13);
+    float f;
+    __builtin_memcpy(&f, &x, 4);
+    return f;
+}
+static inline uint16_t f2bf(float f) {  // round-to-nearest-even, NaN kept NaN
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace wm

@@ -1,0 +1,841 @@
+// The MI355X Whisper engine: workspace, encoder/decoder forward on one HIP stream, and the
+// batched window scheduler that reproduces whisper_full_with_state for every clip of a batch
+// (reference call site whisper.rs:127-129).
+//
+// Control flow is whisper.cpp's [ext], restated in oracle/oracle_whisper.cpp `full()` and kept
+// per clip here (prompt/temperature/seek/segments live on the host, one small struct per clip);
+// the arithmetic is batched across clips: one encoder pass per group of windows, one cross-KV
+// GEMM, a ragged prefill, then lockstep decode steps over every clip still decoding. Per step the
+// host receives only a 32-byte TokOut per clip (plus the probs row of clips that sample at t>0).
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "engine.h"
+
+namespace wm {
+
+static size_t esize(DType) { return 2; }
+
+static void dfree(void* p) { if (p) WM_CHECK(hipFree(p)); }
+
+// ---- live kernel timing (HIP events on the state's stream) ------------------------------------------
+static hipEvent_t kt_event(whisper_state* s) {
+    if (!s->kpool.empty()) { hipEvent_t e = s->kpool.back(); s->kpool.pop_back(); return e; }
+    hipEvent_t e;
+    WM_CHECK(hipEventCreate(&e));
+    return e;
+}
+struct KT {
+    whisper_state* s;
+    int cls;
+    double work;
+    hipEvent_t a = nullptr;
+    KT(whisper_state* s_, int c, double w) : s(s_), cls(c), work(w) {
+        if ((s->ktime_mask >> c) & 1) { a = kt_event(s); WM_CHECK(hipEventRecord(a, s->stream)); }
+    }
+    ~KT() {
+        if (!a) return;
+        hipEvent_t b = kt_event(s);
+        WM_CHECK(hipEventRecord(b, s->stream));
+        s->kpending.push_back({cls, a, b, work});
+    }
+};
+void kt_flush(whisper_state* s) {
+    if (s->kpending.empty()) return;
+    WM_CHECK(hipStreamSynchronize(s->stream));
+    for (auto& p : s->kpending) {
+        float ms = 0.0f;
+        WM_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        s->kstat[p.cls].ms += ms;
+        s->kstat[p.cls].work += p.work;
+        s->kstat[p.cls].count++;
+        s->kpool.push_back(p.a);
+        s->kpool.push_back(p.b);
+    }
+    s->kpending.clear();
+}
+// GEMM launch with its algorithmic work: FLOPs for encoder-side GEMMs (MFMA-bound), HBM bytes
+// (weights + activations) for decode-side GEMMs (weight-streaming)
+static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g, hipStream_t st) {
+    const double work = cls == K_GEMM_ENC ? 2.0 * g.M * g.N * g.K
+                                          : 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N;
+    KT kt(s, cls, work);
+    launch_gemm(dt, epi, g, st);
+}
+
+whisper_state* new_state(Context* c) {
+    WM_CHECK(hipSetDevice(c->device));
+    whisper_state* s = new whisper_state();
+    s->ctx = c;
+    WM_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    return s;
+}
+
+static void free_ws(Workspace& w) {
+    // sub-allocations (pos/slot/.. of tok, win_seek/win_slot of win_job, pcm_ptrs/n_* of mel_ptrs)
+    // are freed with their parent
+    void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
+                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs};
+    for (void* p : ps) dfree(p);
+    if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
+    if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
+    if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
+    w = Workspace();
+}
+
+void free_state(whisper_state* s) {
+    if (!s) return;
+    hipSetDevice(s->ctx->device);
+    hipStreamSynchronize(s->stream);
+    free_ws(s->ws);
+    hipStreamDestroy(s->stream);
+    delete s;
+}
+
+static int enc_batch_cap() {
+    const char* e = getenv("WHISPER_MI355X_ENC_BATCH");
+    int v = e ? atoi(e) : 32;
+    return v > 0 ? v : 32;
+}
+
+// (Re)allocate the workspace for n_jobs clips. Encoder activations are sized for at most
+// enc_batch_cap() windows at once; caches for n_jobs slots.
+static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
+    Workspace& w = s->ws;
+    const Hparams& hp = c->hp;
+    const size_t d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, E = esize(c->dt);
+    const int n_enc = std::min(n_jobs, enc_batch_cap());
+    size_t unused = 0;
+    if (n_enc > w.cap_enc) {
+        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job}) dfree(p);
+        WM_CHECK(hipMalloc(&w.mel_img, (size_t)n_enc * 3002 * nm * E));
+        WM_CHECK(hipMalloc(&w.h1, (size_t)n_enc * 3002 * d * E));
+        WM_CHECK(hipMemset(w.h1, 0, (size_t)n_enc * 3002 * d * E));  // conv padding rows stay zero
+        WM_CHECK(hipMalloc(&w.hn, (size_t)n_enc * T * d * E));
+        WM_CHECK(hipMalloc(&w.qkv, (size_t)n_enc * T * 3 * d * E));
+        WM_CHECK(hipMalloc(&w.att, (size_t)n_enc * T * d * E));
+        WM_CHECK(hipMalloc(&w.ff, (size_t)n_enc * T * 4 * d * E));
+        WM_CHECK(hipMalloc((void**)&w.x, (size_t)n_enc * T * d * 4));
+        WM_CHECK(hipMalloc((void**)&w.win_job, (size_t)n_enc * 3 * sizeof(int)));
+        w.win_seek = w.win_job + n_enc;
+        w.win_slot = w.win_job + 2 * n_enc;
+        w.cap_enc = n_enc;
+    }
+    if (n_jobs > w.cap_jobs) {
+        const int L = hp.n_text_layer;
+        const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
+        for (void* p : {w.cross, w.self, (void*)w.dx, w.dh, w.dq, w.datt, w.dff, w.lrow, (void*)w.logits, (void*)w.probs,
+                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs})
+            dfree(p);
+        if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
+        if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
+        if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
+        WM_CHECK(hipMalloc(&w.cross, (size_t)n_jobs * L * 2 * T * d * E));
+        WM_CHECK(hipMalloc(&w.self, (size_t)n_jobs * L * 2 * hp.n_text_ctx * d * E));
+        WM_CHECK(hipMalloc((void**)&w.dx, (size_t)n_tok * d * 4));
+        WM_CHECK(hipMalloc(&w.dh, (size_t)n_tok * d * E));
+        WM_CHECK(hipMalloc(&w.dq, (size_t)n_tok * d * E));
+        WM_CHECK(hipMalloc(&w.datt, (size_t)n_tok * d * E));
+        WM_CHECK(hipMalloc(&w.dff, (size_t)n_tok * 4 * d * E));
+        WM_CHECK(hipMalloc(&w.lrow, (size_t)n_jobs * d * E));
+        WM_CHECK(hipMalloc((void**)&w.logits, (size_t)n_jobs * hp.n_vocab * 4));
+        WM_CHECK(hipMalloc((void**)&w.probs, (size_t)n_jobs * 2 * hp.n_vocab * 4));
+        WM_CHECK(hipMalloc((void**)&w.tok, ((size_t)5 * n_tok + n_jobs) * sizeof(int)));
+        w.pos = w.tok + n_tok;
+        w.slot = w.tok + 2 * n_tok;
+        w.nkv_self = w.tok + 3 * n_tok;
+        w.nkv_cross = w.tok + 4 * n_tok;
+        w.lrows = w.tok + 5 * n_tok;
+        WM_CHECK(hipMalloc((void**)&w.ctl, (size_t)n_jobs * sizeof(SeqCtl)));
+        WM_CHECK(hipMalloc((void**)&w.tout, (size_t)n_jobs * sizeof(TokOut)));
+        WM_CHECK(hipMalloc((void**)&w.mel_ptrs, (size_t)n_jobs * (2 * sizeof(void*) + 3 * sizeof(int))));
+        w.pcm_ptrs = (const float**)(w.mel_ptrs + n_jobs);
+        w.n_samp = (int*)(w.pcm_ptrs + n_jobs);
+        w.n_len = w.n_samp + n_jobs;
+        w.mel_max = w.n_len + n_jobs;
+        WM_CHECK(hipHostMalloc((void**)&w.h_ints, ((size_t)5 * n_tok + n_jobs) * sizeof(int) + 64, 0));
+        WM_CHECK(hipHostMalloc((void**)&w.h_tout, (size_t)n_jobs * sizeof(TokOut), 0));
+        WM_CHECK(hipHostMalloc((void**)&w.h_ctl, (size_t)n_jobs * sizeof(SeqCtl), 0));
+        w.cap_jobs = n_jobs;
+        w.cap_tok = n_tok;
+    }
+    (void)unused;
+}
+
+// ---- mel ------------------------------------------------------------------------------------------
+static inline int mel_n_len(int n) { return (n + 16000 * 30) / 160; }
+static inline int mel_n_len_org(int n) { return 1 + (int)(((int64_t)n + 200 - 400) / 160); }
+
+int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int* n, int n_jobs, bool on_device) {
+    ensure_ws(c, s, n_jobs);
+    Workspace& w = s->ws;
+    const int nm = c->hp.n_mels;
+    size_t pcm_tot = 0, mel_tot = 0;
+    int max_frames = 1;
+    for (int j = 0; j < n_jobs; j++) {
+        pcm_tot += ((size_t)n[j] + 63) & ~(size_t)63;
+        mel_tot += (size_t)nm * mel_n_len(n[j]);
+        max_frames = std::max(max_frames, std::min((n[j] + 200) / 160 + 1, mel_n_len(n[j])));
+    }
+    if (!on_device && pcm_tot > w.cap_pcm) {
+        dfree(w.pcm);
+        WM_CHECK(hipMalloc((void**)&w.pcm, pcm_tot * 4));
+        w.cap_pcm = pcm_tot;
+    }
+    if (mel_tot > w.cap_mel) {
+        dfree(w.mel);
+        WM_CHECK(hipMalloc((void**)&w.mel, mel_tot * 4));
+        w.cap_mel = mel_tot;
+    }
+    std::vector<const float*> pp(n_jobs);
+    std::vector<float*> mp(n_jobs);
+    std::vector<int> ints(3 * n_jobs);
+    size_t po = 0, mo = 0;
+    for (int j = 0; j < n_jobs; j++) {
+        if (on_device) pp[j] = pcm[j];
+        else {
+            pp[j] = w.pcm + po;
+            if (n[j] > 0) WM_CHECK(hipMemcpyAsync(w.pcm + po, pcm[j], (size_t)n[j] * 4, hipMemcpyHostToDevice, s->stream));
+            po += ((size_t)n[j] + 63) & ~(size_t)63;
+        }
+        mp[j] = w.mel + mo;
+        mo += (size_t)nm * mel_n_len(n[j]);
+        ints[j] = n[j];
+        ints[n_jobs + j] = mel_n_len(n[j]);
+    }
+    // one host block -> device: [mel ptrs][pcm ptrs][n][n_len][max]
+    std::vector<char> blk(n_jobs * (2 * sizeof(void*) + 3 * sizeof(int)));
+    memcpy(blk.data(), mp.data(), n_jobs * sizeof(void*));
+    memcpy(blk.data() + n_jobs * sizeof(void*), pp.data(), n_jobs * sizeof(void*));
+    memcpy(blk.data() + 2 * n_jobs * sizeof(void*), ints.data(), 2 * n_jobs * sizeof(int));
+    WM_CHECK(hipMemcpyAsync(w.mel_ptrs, blk.data(), blk.size() - n_jobs * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    {
+        double bytes = 0;
+        for (int j = 0; j < n_jobs; j++)
+            bytes += 4.0 * n[j] + 4.0 * nm * std::min((n[j] + 200) / 160 + 1, mel_n_len(n[j]));
+        KT kt(s, K_MEL, bytes);
+        launch_mel(w.pcm_ptrs, w.n_samp, c->w.mel_tab, c->w.filt_t, nm, w.mel_ptrs, w.n_len, w.mel_max, n_jobs, max_frames,
+                   s->stream);
+    }
+    WM_CHECK(hipStreamSynchronize(s->stream));  // blk (pageable) must outlive the copy
+    s->n_len = mel_n_len(n[0]);
+    s->n_len_org = mel_n_len_org(n[0]);
+    return 0;
+}
+
+// ---- encoder + cross KV ---------------------------------------------------------------------------
+static GemmArgs gemm_plain(const void* A, int M, int K, const void* B, int N, const float* bias, void* out, long ldo) {
+    GemmArgs g{};
+    g.A = A; g.a_rpb = M > 0 ? M : 1; g.a_bstride = 0; g.a_rstride = K;
+    g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.out = out; g.ldo = ldo; g.o_rpb = M > 0 ? M : 1; g.o_bstride = 0; g.o_off = 0;
+    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    return g;
+}
+
+int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* seeks, const int* slots, int n_win) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, H = hp.n_audio_head;
+    const DType dt = c->dt;
+    const int KCLS = K_GEMM_ENC;
+    const Weights& W = c->w;
+    hipStream_t st = s->stream;
+    for (int b0 = 0; b0 < n_win; b0 += w.cap_enc) {
+        const int nb = std::min(w.cap_enc, n_win - b0);
+        int* hi = w.h_ints;
+        for (int i = 0; i < nb; i++) { hi[i] = jobs[b0 + i]; hi[nb + i] = seeks[b0 + i]; hi[2 * nb + i] = slots[b0 + i]; }
+        WM_CHECK(hipMemcpyAsync(w.win_job, hi, 3 * nb * sizeof(int), hipMemcpyHostToDevice, st));
+        const int* d_job = w.win_job;
+        const int* d_seek = w.win_job + nb;
+        const int* d_slot = w.win_job + 2 * nb;
+        launch_mel_window(dt, w.mel_ptrs, w.n_len, w.n_samp, w.mel_max, d_job, d_seek, nb, nm, w.mel_img, st);
+        // conv1 (stride 1, pad 1) + GELU -> h1 rows 1..3000 of each 3002-row image
+        {
+            GemmArgs g = gemm_plain(w.mel_img, nb * 2 * T, 3 * nm, W.conv1_w, d, W.conv1_b, w.h1, d);
+            g.a_rpb = 2 * T; g.a_bstride = (long)3002 * nm; g.a_rstride = nm;
+            g.o_rpb = 2 * T; g.o_bstride = 3002; g.o_off = 1;
+            tgemm(s, KCLS, dt, EPI_GELU, g, st);
+        }
+        // conv2 (stride 2, pad 1) + GELU + positional embedding -> residual stream x (f32)
+        {
+            GemmArgs g = gemm_plain(w.h1, nb * T, 3 * d, W.conv2_w, d, W.conv2_b, w.x, d);
+            g.a_rpb = T; g.a_bstride = (long)3002 * d; g.a_rstride = 2 * d;
+            g.pos = W.pos_e; g.pos_rows = T;
+            tgemm(s, KCLS, dt, EPI_GELU_POS, g, st);
+        }
+        const int M = nb * T;
+        for (int l = 0; l < hp.n_audio_layer; l++) {
+            const LayerW& L = W.enc[l];
+            launch_layernorm(dt, w.x, nullptr, M, d, L.ln1_w, L.ln1_b, w.hn, st);
+            tgemm(s, KCLS, dt, EPI_STORE, gemm_plain(w.hn, M, d, L.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), st);
+            {
+                KT kt(s, K_ATTN_ENC, 4.0 * nb * H * (double)T * T * 64);
+                launch_attn_encoder(dt, w.qkv, w.att, nb, T, d, H, st);
+            }
+            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
+            launch_layernorm(dt, w.x, nullptr, M, d, L.ln2_w, L.ln2_b, w.hn, st);
+            tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.hn, M, d, L.w1, 4 * d, L.b1, w.ff, 4 * d), st);
+            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, L.w2, d, L.b2, w.x, d), st);
+        }
+        launch_layernorm(dt, w.x, nullptr, M, d, W.lnpost_w, W.lnpost_b, w.hn, st);
+        // cross K/V of every decoder layer in one GEMM, scattered into each window's slot
+        {
+            GemmArgs g = gemm_plain(w.hn, M, d, W.wkv_cross, 2 * hp.n_text_layer * d, W.bkv_cross, nullptr, 0);
+            g.scale = c->k_scale;
+            g.cache = w.cross; g.row_slot = d_slot; g.L = hp.n_text_layer; g.H = hp.n_text_head; g.ctx = T; g.d = d;
+            tgemm(s, KCLS, dt, EPI_CROSSKV, g, st);
+        }
+        WM_CHECK(hipStreamSynchronize(st));  // h_ints reused by the next micro-batch
+    }
+    s->last_enc_windows = n_win;
+    return 0;
+}
+
+// ---- decoder --------------------------------------------------------------------------------------
+// n_tok tokens (ragged over slots) -> logits of n_rows rows (row r = token lrows[r]) into w.logits.
+// Token metadata must already be in w.h_ints: [tok | pos | slot | - | - ] with stride cap_tok and
+// lrows at 5*cap_tok.
+static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
+    const DType dt = c->dt;
+    const Weights& W = c->w;
+    hipStream_t st = s->stream;
+    int* hi = w.h_ints;
+    const int ct = w.cap_tok;
+    const int KCLS = K_GEMM_DEC;
+    double self_kv = 0;
+    for (int i = 0; i < n_tok; i++) {
+        hi[3 * ct + i] = hi[ct + i] + 1;
+        hi[4 * ct + i] = hp.n_audio_ctx;
+        self_kv += hi[ct + i] + 1;
+    }
+    const double kvrow = (double)H * 64 * 2 * 2;  // K and V row bytes of one position, all heads
+    WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, st));
+    launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
+    for (int l = 0; l < L; l++) {
+        const LayerW& Lw = W.dec[l];
+        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.ln1_w, Lw.ln1_b, w.dh, st);
+        {
+            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wqkv, 3 * d, Lw.bqkv, w.dq, d);
+            g.scale = c->k_scale;
+            g.cache = w.self; g.row_slot = w.slot; g.row_pos = w.pos; g.L = L; g.layer = l; g.H = H;
+            g.ctx = hp.n_text_ctx; g.d = d;
+            tgemm(s, KCLS, dt, EPI_QKV_DEC, g, st);
+        }
+        {
+            KT kt(s, K_ATTN_SELF, self_kv * kvrow);
+            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
+        }
+        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.datt, n_tok, d, Lw.wo, d, Lw.bo, w.dx, d), st);
+        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.lnx_w, Lw.lnx_b, w.dh, st);
+        {
+            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
+            g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
+            tgemm(s, KCLS, dt, EPI_STORE, g, st);
+        }
+        {
+            KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);
+            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
+        }
+        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.datt, n_tok, d, Lw.wxo, d, Lw.bxo, w.dx, d), st);
+        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.ln2_w, Lw.ln2_b, w.dh, st);
+        tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, w.dff, 4 * d), st);
+        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.dff, n_tok, 4 * d, Lw.w2, d, Lw.b2, w.dx, d), st);
+    }
+    launch_layernorm(dt, w.dx, w.lrows, n_rows, d, W.lnd_w, W.lnd_b, w.lrow, st);
+    tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+}
+
+int decode_tokens(Context* c, whisper_state* s, const int* tokens, const int* pos, const int* slots, int n_tok,
+                  const int* logit_rows, int n_logit_rows) {
+    Workspace& w = s->ws;
+    if (n_tok > w.cap_tok) return -1;
+    int* hi = w.h_ints;
+    for (int i = 0; i < n_tok; i++) { hi[i] = tokens[i]; hi[w.cap_tok + i] = pos[i]; hi[2 * w.cap_tok + i] = slots[i]; }
+    for (int r = 0; r < n_logit_rows; r++) hi[5 * w.cap_tok + r] = logit_rows[r];
+    decoder_forward(c, s, n_tok, n_logit_rows);
+    return 0;
+}
+
+// ---- scheduler ------------------------------------------------------------------------------------
+enum Phase { PH_ENCODE, PH_LANG, PH_PREFILL, PH_DECODE, PH_DONE };
+
+struct Job {
+    int slot = 0;
+    int n_samples = 0, n_len = 0, n_len_org = 0;
+    int seek = 0, seek_start = 0, seek_end = 0;
+    bool lang_pending = false;
+    int lang_id = 0;
+    std::vector<int> prompt_init, prompt_past, prompt;
+    int temp_idx = 0;
+    std::vector<TokenData> tokens;
+    int result_len = 0;
+    double sum_logprobs_all = 0, sum_logprobs = -INFINITY, avg_logprobs = -INFINITY, entropy = 0, score = -INFINITY;
+    int seek_delta = 3000;
+    bool has_ts = false, failed = false, completed = false;
+    int step = 0;
+    float no_speech_prob = 0.0f;
+    std::mt19937* rng = nullptr;
+    std::mt19937 own_rng{0};
+    Phase phase = PH_ENCODE;
+    std::vector<Segment> result;
+    int n_new_segments = 0;
+};
+
+struct Sched {
+    Context* c;
+    whisper_state* s;
+    whisper_full_params p;
+    FullOpts o;
+    std::vector<float> temps;
+    std::vector<Job> jobs;
+    bool single_api;
+    int n_max_steps;
+    long decoded = 0;
+    double t_mel = 0, t_enc = 0, t_prefill = 0, t_decode = 0, t_logits = 0;
+};
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static void score_seq(const whisper_full_params& p, Job& j) {
+    if (j.result_len == 0) return;
+    double result = 0.0;
+    for (int i = 0; i < j.result_len; ++i) result += j.tokens[i].plog;
+    j.sum_logprobs = result;
+    j.avg_logprobs = result / j.result_len;
+    double penalty = j.result_len;
+    if (p.length_penalty > 0.0f) penalty = pow((5.0 + penalty) / 6.0, p.length_penalty);
+    j.score = result / penalty;
+    std::map<int, int> counts;
+    int cnt = 0;
+    for (int i = std::max(0, j.result_len - 32); i < j.result_len; ++i) { counts[j.tokens[i].id]++; cnt++; }
+    double entropy = 0.0;
+    for (auto& kv : counts) { const double q = kv.second / (double)cnt; entropy -= q * log(q); }
+    j.entropy = entropy;
+}
+
+static void start_attempt(Sched& S, Job& j) {
+    const Vocab& v = S.c->vocab;
+    const float t = S.temps[j.temp_idx];
+    j.tokens.clear();
+    j.result_len = 0;
+    j.sum_logprobs_all = 0;
+    j.sum_logprobs = j.avg_logprobs = j.score = -INFINITY;
+    j.entropy = 0;
+    j.seek_delta = 100 * WHISPER_CHUNK_SIZE;
+    j.failed = j.completed = j.has_ts = false;
+    j.step = 0;
+    j.prompt.clear();
+    if (!j.prompt_past.empty() && t < 0.5f && S.p.n_max_text_ctx > 0) {
+        const int n_take = std::min(std::min(S.p.n_max_text_ctx, S.c->hp.n_text_ctx / 2), (int)j.prompt_past.size());
+        j.prompt = {v.token_prev};
+        j.prompt.insert(j.prompt.begin() + 1, j.prompt_past.end() - n_take, j.prompt_past.end());
+    }
+    j.prompt.insert(j.prompt.end(), j.prompt_init.begin(), j.prompt_init.end());
+}
+
+static void fill_ctl(Sched& S, Job& j, SeqCtl& ctl, bool want_nosp) {
+    const Vocab& v = S.c->vocab;
+    const float t = S.temps[j.temp_idx];
+    ctl.is_initial = j.tokens.empty();
+    ctl.last_ts = j.tokens.size() > 0 && j.tokens.back().id >= v.token_beg;
+    ctl.penult_ts = j.tokens.size() < 2 || j.tokens[j.tokens.size() - 2].id >= v.token_beg;
+    ctl.has_ts = j.has_ts;
+    ctl.seek_delta = j.seek_delta;
+    ctl.temperature = t;
+    ctl.suppress_blank = S.p.suppress_blank;
+    ctl.no_timestamps = S.p.no_timestamps;
+    ctl.suppress_eot = S.o.fixed_tokens > 0;
+    if (S.p.max_initial_ts > 0.0f) {
+        const float precision = float(WHISPER_CHUNK_SIZE) / S.c->hp.n_audio_ctx;
+        ctl.tid0_initial = (int)std::round(S.p.max_initial_ts / precision);
+    } else ctl.tid0_initial = -1;
+    ctl.want_probs = t >= 1e-6f;
+    ctl.want_nosp = want_nosp;
+}
+
+static void finish_window(Sched& S, Job& j) {
+    const Vocab& v = S.c->vocab;
+    const whisper_full_params& p = S.p;
+    const int seek_delta = j.seek_delta;
+    const int result_len = j.result_len;
+    const auto& toks = j.tokens;
+    const bool is_no_speech = (j.no_speech_prob > p.no_speech_thold && j.avg_logprobs < p.logprob_thold);
+    std::vector<int> past;
+    if (j.prompt.front() == v.token_prev)
+        past.insert(past.end(), j.prompt.begin() + 1, j.prompt.end() - j.prompt_init.size());
+    for (int i = 0; i < result_len && !is_no_speech && i < (int)toks.size(); ++i) past.push_back(toks[i].id);
+    j.prompt_past.swap(past);
+    const size_t n_before = j.result.size();
+    if (!toks.empty() && !is_no_speech) {
+        int i0 = 0;
+        int64_t t0 = j.seek + 2 * (toks.front().tid - v.token_beg);
+        std::string text;
+        for (int i = 0; i < (int)toks.size(); i++) {
+            if (p.print_special || toks[i].id < v.token_eot) text += v.id_to_token[toks[i].id];
+            if (toks[i].id > v.token_beg && !p.single_segment) {
+                const int64_t t1 = j.seek + 2 * (toks[i].tid - v.token_beg);
+                if (!text.empty()) {
+                    j.result.push_back({t0, t1, text, j.no_speech_prob, {}});
+                    for (int k = i0; k <= i; k++) j.result.back().tokens.push_back(toks[k]);
+                }
+                text = "";
+                while (i < (int)toks.size() && toks[i].id > v.token_beg) i++;
+                i--;
+                t0 = t1;
+                i0 = i + 1;
+            }
+        }
+        if (!text.empty()) {
+            const int64_t t1 = j.seek + seek_delta;
+            j.result.push_back({t0, t1, text, j.no_speech_prob, {}});
+            for (int k = i0; k < (int)toks.size(); k++) j.result.back().tokens.push_back(toks[k]);
+        }
+    }
+    j.n_new_segments = (int)(j.result.size() - n_before);
+    j.seek += seek_delta;
+    j.phase = (j.seek + 10 >= j.seek_end) ? PH_DONE : PH_ENCODE;
+}
+
+static void attempt_done(Sched& S, Job& j) {
+    if (!j.failed) {
+        j.tokens.resize(j.result_len);
+        score_seq(S.p, j);
+        if (j.result_len > 32 && j.entropy < S.p.entropy_thold) j.failed = true;
+    }
+    bool success = true;
+    if (j.temp_idx != (int)S.temps.size() - 1)
+        if (j.failed || j.avg_logprobs < S.p.logprob_thold) success = false;
+    if (!success) {
+        j.temp_idx++;
+        j.phase = PH_PREFILL;
+        return;
+    }
+    finish_window(S, j);
+}
+
+// one whisper_full "sample + update" iteration for token index j.step; returns true if decoding continues
+static bool process_step(Sched& S, Job& j, const TokOut& r, const float* probs_row) {
+    const Vocab& v = S.c->vocab;
+    const whisper_full_params& p = S.p;
+    const int i = j.step;
+    const float t = S.temps[j.temp_idx];
+    TokenData td;
+    td.tid = r.tid; td.pt = r.pt; td.ptsum = r.ptsum;
+    if (t < 1e-6f) {
+        td.id = r.id; td.p = r.p; td.plog = r.plog;
+    } else {
+        const int n = v.n_vocab;
+        std::discrete_distribution<> dist(probs_row, probs_row + n);
+        td.id = dist(*j.rng);
+        td.p = probs_row[td.id];
+        td.plog = probs_row[n + td.id];
+        if (td.id >= v.token_beg) { td.tid = td.id; td.pt = td.p; }
+        else { td.tid = r.tid; td.pt = r.pt; }
+    }
+    j.tokens.push_back(td);
+    j.sum_logprobs_all += td.plog;
+    S.decoded++;
+    const int delta_min = 10;
+    if (td.id > v.token_beg) {
+        const int sd_new = 2 * (td.id - v.token_beg);
+        if (j.has_ts && j.seek_delta > sd_new && j.result_len < i && S.o.fixed_tokens <= 0) {
+            j.failed = true;
+            return false;
+        }
+        j.seek_delta = sd_new;
+        j.result_len = i + 1;
+        j.has_ts = true;
+    }
+    if (S.o.fixed_tokens > 0) {
+        if (i == S.n_max_steps - 1) { j.result_len = S.n_max_steps; j.completed = true; return false; }
+    } else if (td.id == v.token_eot || (p.max_tokens > 0 && i >= p.max_tokens) ||
+               (j.has_ts && j.seek + j.seek_delta + delta_min >= j.seek_end)) {
+        if (j.result_len == 0 && !p.no_timestamps) {
+            if (j.seek + j.seek_delta + delta_min >= j.seek_end) j.result_len = i + 1;
+            else { j.failed = true; return false; }
+        }
+        if (p.single_segment || p.no_timestamps) { j.result_len = i + 1; j.seek_delta = 100 * WHISPER_CHUNK_SIZE; }
+        j.completed = true;
+        return false;
+    }
+    if (S.o.fixed_tokens <= 0 && i == S.n_max_steps - 1 &&
+        (j.result_len == 0 || j.seek_delta < 100 * WHISPER_CHUNK_SIZE / 2)) {
+        j.failed = true;
+        return false;
+    }
+    // whisper.cpp's loop runs i < n_max: after the last iteration nothing more is sampled (its
+    // trailing decode cannot change the result, so it is skipped here)
+    if (i + 1 >= S.n_max_steps) return false;
+    return true;
+}
+
+// logits kernel over the rows of `act` jobs (row r of w.logits belongs to act[r]) + D2H
+static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, std::vector<std::vector<float>>& probs_rows) {
+    Context* c = S.c;
+    Workspace& w = S.s->ws;
+    hipStream_t st = S.s->stream;
+    const int n = (int)act.size();
+    bool any_probs = false;
+    for (int r = 0; r < n; r++) {
+        fill_ctl(S, S.jobs[act[r]], w.h_ctl[r], want_nosp);
+        any_probs |= w.h_ctl[r].want_probs != 0;
+    }
+    WM_CHECK(hipMemcpyAsync(w.ctl, w.h_ctl, n * sizeof(SeqCtl), hipMemcpyHostToDevice, st));
+    {
+        KT kt(S.s, K_LOGITS, (double)n * c->hp.n_vocab * 4);
+        launch_logits(w.logits, c->hp.n_vocab, w.ctl, n, c->vid, w.tout, w.probs, st);
+    }
+    WM_CHECK(hipMemcpyAsync(w.h_tout, w.tout, n * sizeof(TokOut), hipMemcpyDeviceToHost, st));
+    probs_rows.assign(n, {});
+    if (any_probs) {  // sampling clips (t > 0): probs and logprobs rows for std::discrete_distribution
+        const size_t V = c->hp.n_vocab;
+        for (int r = 0; r < n; r++)
+            if (w.h_ctl[r].want_probs) {
+                probs_rows[r].resize(2 * V);
+                WM_CHECK(hipMemcpyAsync(probs_rows[r].data(), w.probs + (size_t)r * 2 * V, 2 * V * 4, hipMemcpyDeviceToHost, st));
+            }
+    }
+    WM_CHECK(hipStreamSynchronize(st));
+}
+
+int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
+               int n_jobs, bool on_device, const FullOpts& o, bool single_api) {
+    WM_CHECK(hipSetDevice(c->device));
+    if (p.strategy != WHISPER_SAMPLING_GREEDY || p.greedy.best_of > 1) {
+        fprintf(stderr, "whisper_mi355x: only greedy best_of=1 (the reference's strategy, whisper.rs:88) is implemented\n");
+        return -100;
+    }
+    Sched S;
+    S.c = c; S.s = s; S.p = p; S.o = o; S.single_api = single_api;
+    const Vocab& v = c->vocab;
+    const Hparams& hp = c->hp;
+    s->results.assign(n_jobs, {});
+    s->lang_ids.assign(n_jobs, 0);
+    s->decoded_tokens = 0;
+    double t0 = now_ms();
+    ensure_ws(c, s, n_jobs);
+    compute_mel(c, s, pcm, n, n_jobs, on_device);
+    S.t_mel = now_ms() - t0;
+
+    if (p.temperature_inc > 0.0f && o.fixed_tokens <= 0)
+        for (float t = p.temperature; t < 1.0f + 1e-6f; t += p.temperature_inc) S.temps.push_back(t);
+    else S.temps.push_back(p.temperature);
+    const int n_max = hp.n_text_ctx / 2 - 4;
+    S.n_max_steps = o.fixed_tokens > 0 ? o.fixed_tokens : n_max;
+    const bool need_lang = p.language == nullptr || strlen(p.language) == 0 || strcmp(p.language, "auto") == 0 || p.detect_language;
+    std::vector<int> init_prompt_tokens;
+    if (!p.prompt_tokens && p.initial_prompt) init_prompt_tokens = tokenize(v, p.initial_prompt);
+    else if (p.prompt_tokens && p.prompt_n_tokens > 0) init_prompt_tokens.assign(p.prompt_tokens, p.prompt_tokens + p.prompt_n_tokens);
+    const bool is_distil = hp.n_text_layer == 2 && hp.n_vocab != 51866;
+    const bool no_ts = p.no_timestamps || is_distil;
+    S.p.no_timestamps = no_ts;
+
+    S.jobs.resize(n_jobs);
+    for (int k = 0; k < n_jobs; k++) {
+        Job& j = S.jobs[k];
+        j.slot = k;
+        j.n_samples = n[k];
+        j.n_len = mel_n_len(n[k]);
+        j.n_len_org = mel_n_len_org(n[k]);
+        j.seek_start = p.offset_ms / 10;
+        j.seek_end = p.duration_ms == 0 ? j.n_len_org : j.seek_start + p.duration_ms / 10;
+        j.seek = j.seek_start;
+        j.rng = single_api ? &s->rng : &j.own_rng;
+        if (single_api) j.prompt_past = s->prompt_past;
+        if (p.no_context) j.prompt_past.clear();
+        if (!init_prompt_tokens.empty()) {
+            for (int t : init_prompt_tokens) j.prompt_past.push_back(t);
+            std::rotate(j.prompt_past.begin(), j.prompt_past.end() - init_prompt_tokens.size(), j.prompt_past.end());
+        }
+        if (need_lang && 0 >= j.n_len_org) { j.phase = PH_DONE; continue; }  // whisper: lang detect fails -> -3
+        if (j.seek_end < j.seek_start + 10) { j.phase = PH_DONE; continue; }
+        j.lang_pending = need_lang;
+        if (!need_lang) j.lang_id = lang_index(p.language);
+        j.phase = PH_ENCODE;
+    }
+    auto build_prompt_init = [&](Job& j) -> bool {
+        j.prompt_init = {v.token_sot};
+        if (v.is_multilingual()) {
+            if (j.lang_id < 0) return false;
+            j.prompt_init.push_back(v.token_sot + 1 + j.lang_id);
+            j.prompt_init.push_back(p.translate ? v.token_translate : v.token_transcribe);
+        }
+        if (no_ts) j.prompt_init.push_back(v.token_not);
+        return true;
+    };
+    for (auto& j : S.jobs)
+        if (j.phase != PH_DONE && !j.lang_pending && !build_prompt_init(j)) return -7;
+
+    Workspace& w = s->ws;
+    std::vector<std::vector<float>> probs_rows;
+    bool aborted = false;
+    while (!aborted) {
+        bool any = false;
+        for (auto& j : S.jobs) any |= j.phase != PH_DONE;
+        if (!any) break;
+        // ---- encode every window that is due
+        {
+            std::vector<int> wj, ws_, wsl;
+            for (int k = 0; k < n_jobs; k++) {
+                Job& j = S.jobs[k];
+                if (j.phase != PH_ENCODE) continue;
+                if (single_api && p.progress_callback) {
+                    const int prog = (100 * (j.seek - j.seek_start)) / std::max(1, j.seek_end - j.seek_start);
+                    p.progress_callback(c->owner, s, prog, p.progress_callback_user_data);
+                }
+                if (j.seek + 10 >= j.seek_end && !j.lang_pending) { j.phase = PH_DONE; continue; }
+                if (single_api && p.encoder_begin_callback &&
+                    !p.encoder_begin_callback(c->owner, s, p.encoder_begin_callback_user_data)) {
+                    aborted = true;
+                    break;
+                }
+                if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
+                wj.push_back(k);
+                ws_.push_back(j.lang_pending ? 0 : j.seek);
+                wsl.push_back(j.slot);
+            }
+            if (aborted) break;
+            if (!wj.empty()) {
+                const double te = now_ms();
+                encode_windows(c, s, wj.data(), ws_.data(), wsl.data(), (int)wj.size());
+                S.t_enc += now_ms() - te;
+                for (int k : wj) {
+                    Job& j = S.jobs[k];
+                    if (j.lang_pending) { j.phase = PH_LANG; continue; }
+                    if (j.seek > j.seek_start && j.seek + 500 >= j.seek_end) j.prompt_past.clear();
+                    j.temp_idx = 0;
+                    j.phase = PH_PREFILL;
+                }
+            }
+        }
+        // ---- language detection: decode [sot] at pos 0, argmax over the language logits
+        {
+            std::vector<int> act;
+            for (int k = 0; k < n_jobs; k++) if (S.jobs[k].phase == PH_LANG) act.push_back(k);
+            if (!act.empty()) {
+                const double tp = now_ms();
+                const int na = (int)act.size();
+                int* hi = w.h_ints;
+                for (int r = 0; r < na; r++) {
+                    hi[r] = v.token_sot; hi[w.cap_tok + r] = 0; hi[2 * w.cap_tok + r] = S.jobs[act[r]].slot;
+                    hi[5 * w.cap_tok + r] = r;
+                }
+                decoder_forward(c, s, na, na);
+                std::vector<float> lg((size_t)na * 100);
+                for (int r = 0; r < na; r++)
+                    WM_CHECK(hipMemcpyAsync(lg.data() + r * 100, w.logits + (size_t)r * hp.n_vocab + v.token_sot + 1, 100 * 4,
+                                            hipMemcpyDeviceToHost, s->stream));
+                WM_CHECK(hipStreamSynchronize(s->stream));
+                S.t_prefill += now_ms() - tp;
+                for (int r = 0; r < na; r++) {
+                    Job& j = S.jobs[act[r]];
+                    // whisper_lang_auto_detect_with_state: iterate g_lang (std::map, key order), sort desc
+                    std::map<std::string, int> g_lang;
+                    for (int i = 0; i < 100; i++) g_lang[k_lang_codes[i]] = i;
+                    std::vector<std::pair<float, int>> ids;
+                    for (auto& kv : g_lang) ids.emplace_back(lg[r * 100 + kv.second], kv.second);
+                    std::sort(ids.begin(), ids.end(), [](const std::pair<float, int>& a, const std::pair<float, int>& b) { return a.first > b.first; });
+                    j.lang_id = ids[0].second;
+                    j.lang_pending = false;
+                    if (!build_prompt_init(j)) return -7;
+                    if (p.detect_language) { j.phase = PH_DONE; continue; }
+                    if (j.seek == 0) {
+                        j.temp_idx = 0;
+                        j.phase = PH_PREFILL;
+                    } else j.phase = PH_ENCODE;
+                }
+            }
+        }
+        // ---- prefill every attempt that is due
+        {
+            std::vector<int> act;
+            for (int k = 0; k < n_jobs; k++) if (S.jobs[k].phase == PH_PREFILL) act.push_back(k);
+            if (!act.empty()) {
+                if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
+                const double tp = now_ms();
+                int* hi = w.h_ints;
+                int nt = 0;
+                for (int r = 0; r < (int)act.size(); r++) {
+                    Job& j = S.jobs[act[r]];
+                    start_attempt(S, j);
+                    for (int t = 0; t < (int)j.prompt.size(); t++) {
+                        hi[nt] = j.prompt[t]; hi[w.cap_tok + nt] = t; hi[2 * w.cap_tok + nt] = j.slot;
+                        nt++;
+                    }
+                    hi[5 * w.cap_tok + r] = nt - 1;
+                }
+                decoder_forward(c, s, nt, (int)act.size());
+                run_logits(S, act, true, probs_rows);
+                S.t_prefill += now_ms() - tp;
+                for (int r = 0; r < (int)act.size(); r++) {
+                    Job& j = S.jobs[act[r]];
+                    j.no_speech_prob = w.h_tout[r].nosp_prob;
+                    if (process_step(S, j, w.h_tout[r], probs_rows[r].empty() ? nullptr : probs_rows[r].data())) j.phase = PH_DECODE;
+                    else attempt_done(S, j);
+                }
+            }
+        }
+        // ---- one decode step for every clip that is decoding
+        {
+            std::vector<int> act;
+            for (int k = 0; k < n_jobs; k++) if (S.jobs[k].phase == PH_DECODE) act.push_back(k);
+            if (!act.empty()) {
+                if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
+                const double td = now_ms();
+                int* hi = w.h_ints;
+                const int na = (int)act.size();
+                for (int r = 0; r < na; r++) {
+                    Job& j = S.jobs[act[r]];
+                    hi[r] = j.tokens.back().id;
+                    hi[w.cap_tok + r] = (int)j.prompt.size() + j.step;
+                    hi[2 * w.cap_tok + r] = j.slot;
+                    hi[5 * w.cap_tok + r] = r;
+                }
+                decoder_forward(c, s, na, na);
+                run_logits(S, act, false, probs_rows);
+                S.t_decode += now_ms() - td;
+                for (int r = 0; r < na; r++) {
+                    Job& j = S.jobs[act[r]];
+                    j.step++;
+                    if (!process_step(S, j, w.h_tout[r], probs_rows[r].empty() ? nullptr : probs_rows[r].data())) attempt_done(S, j);
+                }
+            }
+        }
+        // ---- new-segment callback (whisper.h single-clip API)
+        if (single_api && p.new_segment_callback) {
+            Job& j = S.jobs[0];
+            if (j.n_new_segments > 0) {
+                s->results[0] = j.result;
+                p.new_segment_callback(c->owner, s, j.n_new_segments,
+                                       p.new_segment_callback_user_data);
+                j.n_new_segments = 0;
+            }
+        }
+    }
+    for (int k = 0; k < n_jobs; k++) {
+        s->results[k] = std::move(S.jobs[k].result);
+        s->lang_ids[k] = S.jobs[k].lang_id;
+    }
+    if (single_api && n_jobs > 0) {
+        s->prompt_past = S.jobs[0].prompt_past;
+        s->lang_id = S.jobs[0].lang_id;
+    }
+    kt_flush(s);
+    s->decoded_tokens = S.decoded;
+    s->phase_ms[0] = S.t_mel; s->phase_ms[1] = S.t_enc; s->phase_ms[2] = S.t_prefill; s->phase_ms[3] = S.t_decode;
+    s->phase_ms[4] = S.t_logits;
+    c->timings.encode_ms += (float)S.t_enc;
+    c->timings.decode_ms += (float)S.t_decode;
+    c->timings.prompt_ms += (float)S.t_prefill;
+    return 0;
+}
+
+}  // namespace wm

@@ -1,0 +1,179 @@
+// Engine internals: model (weights in one HBM arena), vocabulary/tokenizer, per-state workspace,
+// and the batched window scheduler that implements whisper_full semantics for many clips at once.
+#pragma once
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/whisper.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace wm {
+
+struct Hparams {
+    int32_t n_vocab, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
+    int32_t n_text_ctx, n_text_state, n_text_head, n_text_layer, n_mels, ftype;
+};
+
+// whisper.cpp's whisper_vocab semantics (special ids shift for multilingual files, extra
+// tokens synthesised up to n_vocab) — SURVEY.md §8a rows a4, a12.
+struct Vocab {
+    int n_vocab = 51864;
+    int token_eot = 50256, token_sot = 50257, token_translate = 50357, token_transcribe = 50358;
+    int token_solm = 50359, token_prev = 50360, token_nosp = 50361, token_not = 50362, token_beg = 50363;
+    std::map<std::string, int> token_to_id;
+    std::vector<std::string> id_to_token;
+    bool is_multilingual() const { return n_vocab >= 51865; }
+    int num_languages() const { return n_vocab - 51765 - (is_multilingual() ? 1 : 0); }
+};
+
+extern const char* const k_lang_codes[100];
+extern const char* const k_lang_names[100];
+int lang_index(const char* code);
+std::vector<int> tokenize(const Vocab& v, const std::string& text);
+
+struct LayerW {
+    float *ln1_w, *ln1_b;
+    void* wqkv; float* bqkv;
+    void* wo; float* bo;
+    float *lnx_w, *lnx_b;     // decoder cross-attn LN
+    void* wxq; float* bxq;    // decoder cross-attn query
+    void* wxo; float* bxo;    // decoder cross-attn out
+    float *ln2_w, *ln2_b;
+    void* w1; float* b1;
+    void* w2; float* b2;
+};
+
+struct Weights {
+    void* conv1_w; float* conv1_b;
+    void* conv2_w; float* conv2_b;
+    float* pos_e;
+    float *lnpost_w, *lnpost_b;
+    void* tok_emb; float* pos_d;
+    float *lnd_w, *lnd_b;
+    void* wkv_cross; float* bkv_cross;  // [L_d][2][d][d], bias [L_d][2][d] (K part zero)
+    std::vector<LayerW> enc, dec;
+    void* mel_tab;    // MelTablesDev (sin, cos, hann)
+    float* filt_t;    // [201][n_mels]
+};
+
+struct Context {
+    Hparams hp;
+    Vocab vocab;
+    VocabIds vid;
+    DType dt = DType::F16;
+    int device = 0;
+    std::string path;
+    int filt_n_mel = 0, filt_n_fft = 0;
+    std::vector<float> filters;
+    Weights w;
+    char* arena = nullptr;
+    size_t arena_bytes = 0;
+    whisper_timings timings{};
+    whisper_state* default_state = nullptr;  // whisper_init_from_file_with_params (with state)
+    float k_scale = 0.0f;                    // d_head^-0.25
+    std::string model_type;
+    whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
+};
+
+struct TokenData {
+    int id, tid;
+    float p, plog, pt, ptsum;
+};
+
+struct Segment {
+    int64_t t0, t1;
+    std::string text;
+    float no_speech_prob;
+    std::vector<TokenData> tokens;
+};
+
+// Workspace sized for a batch of up to `cap_jobs` clips; grows on demand, never shrinks.
+struct Workspace {
+    int cap_jobs = 0, cap_enc = 0, cap_tok = 0;
+    size_t cap_mel = 0, cap_pcm = 0;
+    // encoder (cap_enc windows)
+    void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
+    float* x = nullptr;
+    // caches (cap_jobs slots)
+    void *cross = nullptr, *self = nullptr;
+    // decoder (cap_tok tokens)
+    float* dx = nullptr;
+    void *dh = nullptr, *dq = nullptr, *datt = nullptr, *dff = nullptr, *lrow = nullptr;
+    float *logits = nullptr, *probs = nullptr;
+    int *tok = nullptr, *pos = nullptr, *slot = nullptr, *nkv_self = nullptr, *nkv_cross = nullptr, *lrows = nullptr;
+    SeqCtl* ctl = nullptr;
+    TokOut* tout = nullptr;
+    int *win_job = nullptr, *win_seek = nullptr, *win_slot = nullptr;
+    // mel / pcm
+    float* pcm = nullptr;
+    float* mel = nullptr;
+    float** mel_ptrs = nullptr;
+    const float** pcm_ptrs = nullptr;
+    int *n_samp = nullptr, *n_len = nullptr, *mel_max = nullptr;
+    // host pinned staging
+    int* h_ints = nullptr;
+    TokOut* h_tout = nullptr;
+    SeqCtl* h_ctl = nullptr;
+};
+
+struct Job;
+
+// Live per-kernel-class timing with HIP events on the state's stream (bench.py's roofline leg).
+// `work` is the algorithmic FLOPs (MFMA-bound classes) or HBM bytes (HBM-bound classes).
+enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_OTHER, K_NCLASS };
+struct KStat { double ms = 0, work = 0; long count = 0; };
+
+}  // namespace wm
+
+struct whisper_state {
+    wm::Context* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    wm::Workspace ws;
+    // whisper.h single-clip results (job 0 of the last call) + batch results
+    std::vector<std::vector<wm::Segment>> results;
+    std::vector<int> lang_ids;
+    std::vector<int> prompt_past;  // persists across whisper_full calls on this state
+    std::mt19937 rng{0};           // decoder 0's rng: created with the state, never reset
+    int lang_id = 0;
+    int n_len = 0, n_len_org = 0;  // last mel
+    std::vector<float> logits_host;
+    double phase_ms[5] = {0, 0, 0, 0, 0};
+    long decoded_tokens = 0;
+    // standalone encode/decode API support
+    int last_enc_windows = 0;
+    // kernel timing (off unless whisper_mi355x_kernel_timing enabled it)
+    int ktime_mask = 0;  // bit k: time kernel class k
+    wm::KStat kstat[wm::K_NCLASS];
+    struct KPending { int cls; hipEvent_t a, b; double work; };
+    std::vector<KPending> kpending;
+    std::vector<hipEvent_t> kpool;
+};
+
+struct whisper_context {
+    wm::Context c;
+};
+
+namespace wm {
+bool load_context(Context* c, const char* path, int device, DType dt, bool load_weights);
+void free_context(Context* c);
+whisper_state* new_state(Context* c);
+void free_state(whisper_state* s);
+
+struct FullOpts {
+    int fixed_tokens = 0;
+};
+// whisper_full over n_jobs clips. B=1 with the state's own prompt_past/rng reproduces
+// whisper_full_with_state; B>1 treats every clip as a fresh state.
+int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
+               int n_jobs, bool on_device, const FullOpts& o, bool single_api);
+
+// pieces exposed for whisper.h's low-level API
+int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int* n, int n_jobs, bool on_device);
+int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* seeks, const int* slots, int n_win);
+int decode_tokens(Context* c, whisper_state* s, const int* tokens, const int* pos, const int* slots, int n_tok,
+                  const int* logit_rows, int n_logit_rows);
+}  // namespace wm

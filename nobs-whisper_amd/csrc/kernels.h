@@ -1,0 +1,70 @@
+// Host-side launchers of the gfx950 kernels. Every launcher takes the stream it runs on and
+// never allocates or synchronises (so a decode step can be captured into a hipGraph).
+#pragma once
+#include "common.h"
+
+namespace wm {
+
+// ---- mel (kernels/mel.hip) ---------------------------------------------------------------------
+void launch_mel(const float* const* d_pcm, const int* d_n, const void* d_tab, const float* d_filt_t, int n_mel,
+                float* const* d_mel, const int* d_nlen, int* d_max, int n_jobs, int max_frames, hipStream_t st);
+void launch_mel_window(DType dt, float* const* d_mel, const int* d_nlen, const int* d_n, const int* d_max,
+                       const int* d_win_job, const int* d_win_seek, int n_win, int n_mel, void* out, hipStream_t st);
+void launch_mel_normalize(const float* d_mel, int nl, int n_samples, const int* d_max, int n_mel, float* out, hipStream_t st);
+
+// ---- layer norm / embedding (kernels/norm.hip) ------------------------------------------------
+// y[i] = LN(x[row(i)]) * w + b, x f32 [.][D] (row stride D), y T [M][D]; row(i) = rows ? rows[i] : i
+void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b,
+                      void* y, hipStream_t st);
+// x[i][:] = tok_emb[tok[i]][:] + pos_emb[pos[i]][:]   (f32 out)
+void launch_embed(DType dt, const void* tok_emb, const float* pos_emb, const int* tok, const int* pos, int n, int D,
+                  float* x, hipStream_t st);
+
+// ---- GEMM (kernels/gemm.hip): C[M][N] = A[M][K] . B[N][K]^T + bias, fused epilogues --------------
+enum Epi : int {
+    EPI_STORE = 0,     // T out[orow][n] = (v) * colscale(n)
+    EPI_GELU = 1,      // T out = gelu_ggml(v)
+    EPI_RESID = 2,     // f32 out[orow][n] = v + out[orow][n]            (residual stream, in place)
+    EPI_GELU_POS = 3,  // f32 out = gelu_ggml(v) + pos[m % pos_rows][n]   (conv2 + positional emb)
+    EPI_F32 = 4,       // f32 out = v                                       (logits)
+    EPI_CROSSKV = 5,   // T scatter into cross cache [slot][L][2][H][ctx][64]; K columns scaled
+    EPI_QKV_DEC = 6,   // n<d: T q[m][n]*scale ; d<=n<2d: K cache (scaled) ; 2d<=n<3d: V cache
+};
+
+struct GemmArgs {
+    const void* A; long a_rpb, a_bstride, a_rstride;  // A row m -> A + (m/a_rpb)*a_bstride + (m%a_rpb)*a_rstride
+    const void* B;                                     // [N][K] row-major
+    const float* bias;                                 // [N] or null
+    int M, N, K;
+    void* out; long ldo; long o_rpb, o_bstride, o_off; // out row = (m/o_rpb)*o_bstride + (m%o_rpb) + o_off
+    const float* pos; int pos_rows;                    // EPI_GELU_POS
+    float scale; int sc_div, sc_mod, sc_lim;           // column n scaled iff ((n/sc_div)%sc_mod) < sc_lim
+    // caches (EPI_CROSSKV / EPI_QKV_DEC)
+    void* cache; const int* row_slot; const int* row_pos; int L, layer, H, ctx, d;
+};
+
+void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
+
+// ---- attention (kernels/attn.hip) --------------------------------------------------------------
+// encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)
+void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int d, int H, hipStream_t st);
+// single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:
+// token i attends keys [0, n_kv[i]) of slot[i]; q [n][q_stride] at head h offset h*64; out [n][d]
+void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
+                        int n, int L, int layer, int H, int ctx, int d, void* out, hipStream_t st);
+
+// ---- logits processing (kernels/logits.hip) ----------------------------------------------------
+struct VocabIds {
+    int n_vocab, eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, space, n_lang;
+};
+struct SeqCtl {             // per-sequence inputs of whisper_process_logits
+    int is_initial, last_ts, penult_ts, has_ts, seek_delta;
+    float temperature;
+    int suppress_blank, no_timestamps, suppress_eot, tid0_initial;  // tid0_initial < 0: no max_initial_ts rule
+    int want_probs, want_nosp;
+};
+struct TokOut { int id, tid; float p, plog, pt, ptsum, nosp_prob, pad; };
+void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v,
+                   TokOut* out, float* probs, hipStream_t st);
+
+}  // namespace wm

@@ -1,0 +1,254 @@
+// Attention kernels.
+//
+// Encoder: flash-style self-attention over the 1500 audio positions, d_head = 64, one workgroup =
+// 64 queries of one (chunk, head), 4 waves x 16 query rows. K tiles are staged in LDS row-major
+// (XOR-swizzled 16-byte chunks) and V tiles transposed, so S = Q.K^T and O += P.V are both
+// v_mfma_f32_16x16x32 with ds_read_b128 operand fetches. Softmax runs online per row (16 lanes
+// per row, xor-shuffle reductions), P is rounded to the MFMA input type before P.V as ggml does.
+// Roofline: MFMA-bound (4*T^2*64 FLOP per head).
+//
+// Decoder: one query per (token, head) over a KV cache [slot][L][2][H][ctx][64] — the self cache
+// (ctx 448, n_kv = pos+1) or the cross cache (ctx 1500). Three phases in one workgroup: scores
+// (8 lanes x 16 B per key row, coalesced 1 KiB per wave-instruction), block softmax in LDS,
+// P.V with 8 lanes per value row. Roofline: HBM-bound, 2 x n_kv x 128 B per (token, head).
+#include "../common.h"
+#include "../kernels.h"
+
+namespace wm {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) attn_enc_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
+    typedef typename Frag<T>::type FT;
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long base = (long)b * Tn;
+    const int ld = 3 * d;
+    __shared__ u32x4 Ks[64 * 8];
+    __shared__ u32x4 Vts[64 * 8];
+    __shared__ u32x4 Ps[4][16 * 8];
+
+    const u32x4 zero = {0, 0, 0, 0};
+    FT qf[2];
+    {
+        const int qrow = qb * 64 + wave * 16 + (lane & 15);
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int ch = s * 4 + (lane >> 4);
+            u32x4 v = qrow < Tn ? *(const u32x4*)(qkv + (base + qrow) * ld + h * 64 + ch * 8) : zero;
+            qf[s] = __builtin_bit_cast(FT, v);
+        }
+    }
+    float m_i[4], l_i[4];
+    f32x4 o[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) { m_i[r] = -INFINITY; l_i[r] = 0.0f; o[r] = (f32x4){0.f, 0.f, 0.f, 0.f}; }
+
+    const int n_kt = (Tn + 63) / 64;
+    T* Vt_el = (T*)Vts;
+    T* P_el = (T*)Ps[wave];
+    for (int kt = 0; kt < n_kt; kt++) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int c = tid + i * 256, key = c >> 3, kc = c & 7;
+            const int kg = kt * 64 + key;
+            u32x4 kv = zero, vv = zero;
+            if (kg < Tn) {
+                kv = *(const u32x4*)(qkv + (base + kg) * ld + d + h * 64 + kc * 8);
+                vv = *(const u32x4*)(qkv + (base + kg) * ld + 2 * d + h * 64 + kc * 8);
+            }
+            Ks[key * 8 + swz(key, kc)] = kv;
+            const T* ve = (const T*)&vv;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int dim = kc * 8 + e;
+                Vt_el[(dim * 8 + swz(dim, key >> 3)) * 8 + (key & 7)] = ve[e];
+            }
+        }
+        __syncthreads();
+        f32x4 sacc[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int row = j * 16 + (lane & 15);
+                const FT kf = __builtin_bit_cast(FT, Ks[row * 8 + swz(row, s * 4 + (lane >> 4))]);
+                sacc[j] = mfma16x16x32(qf[s], kf, sacc[j]);
+            }
+        }
+        float mx[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) mx[r] = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int key = kt * 64 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float v = key < Tn ? sacc[j][r] * 0.125f : -INFINITY;
+                sacc[j][r] = v;
+                mx[r] = fmaxf(mx[r], v);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int o2 = 1; o2 < 16; o2 <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o2));
+        }
+        float alpha[4], rs[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float mn = fmaxf(m_i[r], mx[r]);
+            alpha[r] = __expf(m_i[r] - mn);
+            m_i[r] = mn;
+            rs[r] = 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const T pt = (T)__expf(sacc[j][r] - m_i[r]);
+                rs[r] += (float)pt;
+                const int row = (lane >> 4) * 4 + r, key = j * 16 + (lane & 15);
+                P_el[(row * 8 + swz(row, key >> 3)) * 8 + (key & 7)] = pt;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int o2 = 1; o2 < 16; o2 <<= 1) rs[r] += __shfl_xor(rs[r], o2);
+            l_i[r] = l_i[r] * alpha[r] + rs[r];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) o[j][r] *= alpha[r];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P stores landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int prow = lane & 15;
+            const FT pf = __builtin_bit_cast(FT, Ps[wave][prow * 8 + swz(prow, s * 4 + (lane >> 4))]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int vrow = j * 16 + (lane & 15);
+                const FT vf = __builtin_bit_cast(FT, Vts[vrow * 8 + swz(vrow, s * 4 + (lane >> 4))]);
+                o[j] = mfma16x16x32(pf, vf, o[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int row = qb * 64 + wave * 16 + (lane >> 4) * 4 + r;
+        if (row >= Tn) continue;
+        const float inv = 1.0f / l_i[r];
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[(base + row) * d + h * 64 + j * 16 + (lane & 15)] = (T)(o[j][r] * inv);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
+                                                       const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
+                                                       int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
+    const int i = blockIdx.x, h = blockIdx.y;
+    const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3;  // 32 groups of 8 lanes
+    const int n_kv = n_kv_arr[i];
+    const long s = slot[i];
+    const T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
+    const T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
+    __shared__ float sc[1536];
+    __shared__ float red[256];
+    __shared__ float acc_s[32][65];
+
+    float qv[8];
+    {
+        const u32x4 raw = *(const u32x4*)(q + (long)i * q_stride + h * 64 + lane8 * 8);
+        const T* qe = (const T*)&raw;
+#pragma unroll
+        for (int e = 0; e < 8; e++) qv[e] = (float)qe[e];
+    }
+    // phase 1: scores
+    float lmax = -INFINITY;
+    for (int t = grp; t < n_kv; t += 32) {
+        const u32x4 raw = *(const u32x4*)(K + (long)t * 64 + lane8 * 8);
+        const T* ke = (const T*)&raw;
+        float a = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+        a += __shfl_xor(a, 1);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 4);
+        if (lane8 == 0) sc[t] = a;
+        lmax = fmaxf(lmax, a);
+    }
+    // block max
+    red[tid] = lmax;
+    __syncthreads();
+    for (int o2 = 128; o2 > 0; o2 >>= 1) {
+        if (tid < o2) red[tid] = fmaxf(red[tid], red[tid + o2]);
+        __syncthreads();
+    }
+    const float mx = red[0];
+    __syncthreads();
+    float lsum = 0.0f;
+    for (int t = tid; t < n_kv; t += 256) {
+        const float e = expf(sc[t] - mx);
+        sc[t] = e;
+        lsum += e;
+    }
+    red[tid] = lsum;
+    __syncthreads();
+    for (int o2 = 128; o2 > 0; o2 >>= 1) {
+        if (tid < o2) red[tid] += red[tid + o2];
+        __syncthreads();
+    }
+    const float inv = 1.0f / red[0];
+    for (int t = tid; t < n_kv; t += 256) sc[t] = (float)(T)(sc[t] * inv);  // P rounded as ggml's f16 src1
+    __syncthreads();
+    // phase 3: O = P.V
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] = 0.0f;
+    for (int t = grp; t < n_kv; t += 32) {
+        const u32x4 raw = *(const u32x4*)(V + (long)t * 64 + lane8 * 8);
+        const T* ve = (const T*)&raw;
+        const float p = sc[t];
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc_s[grp][lane8 * 8 + e] = acc[e];
+    __syncthreads();
+    if (tid < 64) {
+        float a = 0.0f;
+        for (int g2 = 0; g2 < 32; g2++) a += acc_s[g2][tid];
+        out[(long)i * d + h * 64 + tid] = (T)a;
+    }
+}
+
+void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st) {
+    dim3 grid(cdiv(Tn, 64), H, B);
+    if (dt == DType::F16) attn_enc_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
+    else attn_enc_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
+}
+
+void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv, int n,
+                        int L, int layer, int H, int ctx, int d, void* out, hipStream_t st) {
+    if (n <= 0) return;
+    if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
+    dim3 grid(n, H);
+    if (dt == DType::F16)
+        attn_dec_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, q_stride, (const half_t*)cache, slot, n_kv, L, layer,
+                                                      H, ctx, d, (half_t*)out);
+    else
+        attn_dec_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)cache, slot, n_kv, L,
+                                                      layer, H, ctx, d, (bf16_t*)out);
+}
+
+}  // namespace wm

@@ -1,0 +1,208 @@
+// MFMA GEMM for every projection of the Whisper graph: C[M][N] = A[M][K] . B[N][K]^T (+bias),
+// f16 or bf16 operands, f32 accumulation (v_mfma_f32_16x16x32_{f16,bf16}), with the graph's
+// elementwise tails fused into the epilogue (bias, GELU, residual add, positional embedding,
+// q/k scaling, KV-cache scatter). SURVEY.md §8a rows a7-a10.
+//
+// Both operands are K-contiguous ("NT"), the natural layout of GGML/PyTorch linear weights, so
+// A and B fragments come from the same LDS image shape: [rows][64 halves] = 8 x 16-byte chunks
+// per row, chunk index XOR-swizzled with (row>>1)&7 so that the 16 lanes of a ds_read_b128 group
+// that read one chunk column of 16 consecutive rows hit 16 distinct 16-byte bank slots.
+// Staging: 16-byte global loads to registers issued one K-tile ahead, written to the other LDS
+// buffer after the MFMAs of the current tile (one barrier per K-tile).
+//
+// A's row addressing is affine per batch (row m -> base + (m/rpb)*bstride + (m%rpb)*rstride) so
+// the conv stem is a plain GEMM over a sliding window of the time-major, zero-padded input:
+// conv1 (stride 1) uses rstride = n_mels, conv2 (stride 2) rstride = 2d, with the weights
+// reordered to [out][tap][in] at load time (implicit im2col, no im2col buffer).
+//
+// Roofline: MFMA-bound for the encoder/cross-KV/prefill shapes (M = B*1500), HBM-bound on the
+// weights for decode steps (M = number of active sequences).
+#include "../common.h"
+#include "../kernels.h"
+
+namespace wm {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int EPI, typename T>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float v) {
+    if (g.bias) v = v + g.bias[n];
+    if constexpr (EPI == EPI_STORE) {
+        if (g.sc_div > 0 && ((n / g.sc_div) % g.sc_mod) < g.sc_lim) v = v * g.scale;
+        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
+        ((T*)g.out)[orow * g.ldo + n] = (T)v;
+    } else if constexpr (EPI == EPI_GELU) {
+        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
+        ((T*)g.out)[orow * g.ldo + n] = (T)gelu_ggml(v);
+    } else if constexpr (EPI == EPI_RESID) {
+        float* o = (float*)g.out + (long)m * g.ldo + n;
+        *o = v + *o;
+    } else if constexpr (EPI == EPI_GELU_POS) {
+        ((float*)g.out)[(long)m * g.ldo + n] = gelu_ggml(v) + g.pos[(long)(m % g.pos_rows) * g.N + n];
+    } else if constexpr (EPI == EPI_F32) {
+        ((float*)g.out)[(long)m * g.ldo + n] = v;
+    } else if constexpr (EPI == EPI_CROSSKV) {
+        const int b = m / g.ctx, t = m % g.ctx;
+        const int l = n / (2 * g.d), kv = (n / g.d) & 1, h = (n % g.d) >> 6, dh = n & 63;
+        if (kv == 0) v = v * g.scale;
+        const long slot = g.row_slot[b];
+        ((T*)g.cache)[((((slot * g.L + l) * 2 + kv) * g.H + h) * g.ctx + t) * 64 + dh] = (T)v;
+    } else if constexpr (EPI == EPI_QKV_DEC) {
+        const int part = n / g.d;
+        if (part == 0) {
+            ((T*)g.out)[(long)m * g.ldo + n] = (T)(v * g.scale);
+        } else {
+            const int kv = part - 1, nn = n - part * g.d, h = nn >> 6, dh = nn & 63;
+            if (kv == 0) v = v * g.scale;
+            const long slot = g.row_slot[m], pos = g.row_pos[m];
+            ((T*)g.cache)[((((slot * g.L + g.layer) * 2 + kv) * g.H + h) * g.ctx + pos) * 64 + dh] = (T)v;
+        }
+    }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g) {
+    typedef typename Frag<T>::type FT;
+    constexpr int BK = 64;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int A_PER_T = BM * 8 / 256, B_PER_T = BN * 8 / 256;
+    static_assert(WM * WN == 4, "4 waves");
+    __shared__ u32x4 lds[2][(BM + BN) * 8];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const T* A = (const T*)g.A;
+    const T* B = (const T*)g.B;
+
+    const T* a_ptr[A_PER_T];
+    int a_lds[A_PER_T], a_k[A_PER_T];
+    bool a_ok[A_PER_T];
+#pragma unroll
+    for (int i = 0; i < A_PER_T; i++) {
+        const int c = tid + i * 256, row = c >> 3, kc = c & 7;
+        const int m = m0 + row;
+        a_ok[i] = m < g.M;
+        const int mm = a_ok[i] ? m : 0;
+        a_ptr[i] = A + (mm / g.a_rpb) * g.a_bstride + (mm % g.a_rpb) * g.a_rstride + kc * 8;
+        a_k[i] = kc * 8;
+        a_lds[i] = row * 8 + (kc ^ ((row >> 1) & 7));
+    }
+    const T* b_ptr[B_PER_T];
+    int b_lds[B_PER_T], b_k[B_PER_T];
+    bool b_ok[B_PER_T];
+#pragma unroll
+    for (int i = 0; i < B_PER_T; i++) {
+        const int c = tid + i * 256, row = c >> 3, kc = c & 7;
+        const int n = n0 + row;
+        b_ok[i] = n < g.N;
+        b_ptr[i] = B + (long)(b_ok[i] ? n : 0) * g.K + kc * 8;
+        b_k[i] = kc * 8;
+        b_lds[i] = BM * 8 + row * 8 + (kc ^ ((row >> 1) & 7));
+    }
+
+    u32x4 ra[A_PER_T], rb[B_PER_T];
+    const u32x4 zero = {0, 0, 0, 0};
+    auto gload = [&](int kt) {
+        const int kb = kt * BK;
+#pragma unroll
+        for (int i = 0; i < A_PER_T; i++)
+            ra[i] = (a_ok[i] && kb + a_k[i] < g.K) ? *(const u32x4*)(a_ptr[i] + kb) : zero;
+#pragma unroll
+        for (int i = 0; i < B_PER_T; i++)
+            rb[i] = (b_ok[i] && kb + b_k[i] < g.K) ? *(const u32x4*)(b_ptr[i] + kb) : zero;
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_PER_T; i++) lds[buf][a_lds[i]] = ra[i];
+#pragma unroll
+        for (int i = 0; i < B_PER_T; i++) lds[buf][b_lds[i]] = rb[i];
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (g.K + BK - 1) / BK;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            FT af[TM], bfr[TN];
+            const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                const int row = wm * WTM + i * 16 + (lane & 15);
+                af[i] = __builtin_bit_cast(FT, lds[cur][row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                const int row = wn * WTN + j * 16 + (lane & 15);
+                bfr[j] = __builtin_bit_cast(FT, lds[cur][BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+#pragma unroll
+                for (int j = 0; j < TN; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
+        if (kt + 1 < nk) sstore(cur ^ 1);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+            if (n >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+            }
+        }
+}
+
+template <typename T, int EPI>
+static void launch_t(const GemmArgs& g, hipStream_t st) {
+    if ((long)g.M * g.N >= 256L * 128 * 128) {
+        dim3 grid(cdiv(g.N, 128), cdiv(g.M, 128));
+        gemm_kernel<T, 128, 128, 2, 2, EPI><<<grid, 256, 0, st>>>(g);
+    } else {
+        dim3 grid(cdiv(g.N, 64), cdiv(g.M, 64));
+        gemm_kernel<T, 64, 64, 2, 2, EPI><<<grid, 256, 0, st>>>(g);
+    }
+}
+
+template <typename T>
+static void launch_dt(int epi, const GemmArgs& g, hipStream_t st) {
+    switch (epi) {
+        case EPI_STORE: launch_t<T, EPI_STORE>(g, st); break;
+        case EPI_GELU: launch_t<T, EPI_GELU>(g, st); break;
+        case EPI_RESID: launch_t<T, EPI_RESID>(g, st); break;
+        case EPI_GELU_POS: launch_t<T, EPI_GELU_POS>(g, st); break;
+        case EPI_F32: launch_t<T, EPI_F32>(g, st); break;
+        case EPI_CROSSKV: launch_t<T, EPI_CROSSKV>(g, st); break;
+        case EPI_QKV_DEC: launch_t<T, EPI_QKV_DEC>(g, st); break;
+        default: fprintf(stderr, "whisper_mi355x: bad epilogue %d\n", epi); abort();
+    }
+}
+
+void launch_gemm(DType dt, int epi, const GemmArgs& g, hipStream_t st) {
+    if (g.M <= 0 || g.N <= 0) return;
+    if (g.K % 8 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0) {
+        fprintf(stderr, "whisper_mi355x: gemm shape not supported (K=%d)\n", g.K);
+        abort();
+    }
+    if (dt == DType::F16) launch_dt<half_t>(epi, g, st);
+    else launch_dt<bf16_t>(epi, g, st);
+}
+
+}  // namespace wm

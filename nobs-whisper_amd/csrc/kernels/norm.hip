@@ -1,0 +1,62 @@
+// LayerNorm (ggml_norm + ggml_mul + ggml_add) and decoder token/position embedding.
+//
+// LayerNorm follows ggml-cpu's arithmetic: mean and variance sums in double, mean/variance
+// rounded to float, scale = 1/sqrtf(var + 1e-5), then (v*scale)*w + b as three separately rounded
+// float ops (this file is compiled with -ffp-contract=off). Output is rounded to the GEMM input
+// type, which is exactly the f16 conversion ggml applies to a matmul's src1.
+// Roofline: HBM-bound, 4 B read + 2 B written per element; one wave per row.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace wm {
+
+template <typename T>
+__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, const int* __restrict__ rows, int M, int D,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        T* __restrict__ y) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= M) return;
+    const long r = rows ? rows[i] : i;
+    const float* xr = x + r * D;
+    double s = 0.0;
+    for (int k = lane; k < D; k += 64) s += (double)xr[k];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = (float)(s / D);
+    double s2 = 0.0;
+    for (int k = lane; k < D; k += 64) { const float v = xr[k] - mean; s2 += (double)(v * v); }
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    const float variance = (float)(s2 / D);
+    const float scale = 1.0f / sqrtf(variance + 1e-5f);
+    T* yr = y + (long)i * D;
+    for (int k = lane; k < D; k += 64) {
+        const float v = xr[k] - mean;
+        float t = v * scale;
+        t = t * w[k];
+        yr[k] = (T)(t + b[k]);
+    }
+}
+
+template <typename T>
+__global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__ pe, const int* __restrict__ tok,
+                             const int* __restrict__ pos, int D, float* __restrict__ x) {
+    const int i = blockIdx.x;
+    const long t = tok[i], p = pos[i];
+    for (int k = threadIdx.x; k < D; k += blockDim.x) x[(long)i * D + k] = (float)te[t * D + k] + pe[p * D + k];
+}
+
+void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b, void* y,
+                      hipStream_t st) {
+    if (M <= 0) return;
+    if (dt == DType::F16) layernorm_kernel<half_t><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (half_t*)y);
+    else layernorm_kernel<bf16_t><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (bf16_t*)y);
+}
+
+void launch_embed(DType dt, const void* te, const float* pe, const int* tok, const int* pos, int n, int D, float* x,
+                  hipStream_t st) {
+    if (n <= 0) return;
+    if (dt == DType::F16) embed_kernel<half_t><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x);
+    else embed_kernel<bf16_t><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x);
+}
+
+}  // namespace wm

@@ -1,0 +1,350 @@
+"""ctypes binding of libwhisper_mi355x.so shaped like the whisper-rs 0.15.1 API the reference uses
+(src-tauri/src/whisper.rs:3): WhisperContextParameters, WhisperContext.new_with_params,
+create_state, FullParams, SamplingStrategy.Greedy, WhisperState.full / full_n_segments /
+get_segment. Python is plumbing here (tests, bench.py); the product is the C ABI + HIP kernels.
+
+Loading fails loudly if the shared library is missing: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libwhisper_mi355x.so")
+ENGINE_LIB_PATH = os.path.join(HERE, "lib", "libnobs_whisper_engine.so")
+
+F16, BF16 = 0, 1
+GREEDY, BEAM_SEARCH = 0, 1
+
+
+class WhisperAheads(C.Structure):
+    _fields_ = [("n_heads", C.c_size_t), ("heads", C.c_void_p)]
+
+
+class WhisperContextParams(C.Structure):
+    _fields_ = [("use_gpu", C.c_bool), ("flash_attn", C.c_bool), ("gpu_device", C.c_int),
+                ("dtw_token_timestamps", C.c_bool), ("dtw_aheads_preset", C.c_int), ("dtw_n_top", C.c_int),
+                ("dtw_aheads", WhisperAheads), ("dtw_mem_size", C.c_size_t)]
+
+
+class _Greedy(C.Structure):
+    _fields_ = [("best_of", C.c_int)]
+
+
+class _Beam(C.Structure):
+    _fields_ = [("beam_size", C.c_int), ("patience", C.c_float)]
+
+
+class VadParams(C.Structure):
+    _fields_ = [("threshold", C.c_float), ("min_speech_duration_ms", C.c_int), ("min_silence_duration_ms", C.c_int),
+                ("max_speech_duration_s", C.c_float), ("speech_pad_ms", C.c_int), ("samples_overlap", C.c_float)]
+
+
+class FullParams(C.Structure):
+    """struct whisper_full_params (include/whisper.h), field for field."""
+    _fields_ = [
+        ("strategy", C.c_int), ("n_threads", C.c_int), ("n_max_text_ctx", C.c_int), ("offset_ms", C.c_int),
+        ("duration_ms", C.c_int),
+        ("translate", C.c_bool), ("no_context", C.c_bool), ("no_timestamps", C.c_bool), ("single_segment", C.c_bool),
+        ("print_special", C.c_bool), ("print_progress", C.c_bool), ("print_realtime", C.c_bool),
+        ("print_timestamps", C.c_bool),
+        ("token_timestamps", C.c_bool), ("thold_pt", C.c_float), ("thold_ptsum", C.c_float), ("max_len", C.c_int),
+        ("split_on_word", C.c_bool), ("max_tokens", C.c_int),
+        ("debug_mode", C.c_bool), ("audio_ctx", C.c_int),
+        ("tdrz_enable", C.c_bool),
+        ("suppress_regex", C.c_char_p),
+        ("initial_prompt", C.c_char_p), ("prompt_tokens", C.c_void_p), ("prompt_n_tokens", C.c_int),
+        ("language", C.c_char_p), ("detect_language", C.c_bool),
+        ("suppress_blank", C.c_bool), ("suppress_nst", C.c_bool),
+        ("temperature", C.c_float), ("max_initial_ts", C.c_float), ("length_penalty", C.c_float),
+        ("temperature_inc", C.c_float), ("entropy_thold", C.c_float), ("logprob_thold", C.c_float),
+        ("no_speech_thold", C.c_float),
+        ("greedy", _Greedy), ("beam_search", _Beam),
+        ("new_segment_callback", C.c_void_p), ("new_segment_callback_user_data", C.c_void_p),
+        ("progress_callback", C.c_void_p), ("progress_callback_user_data", C.c_void_p),
+        ("encoder_begin_callback", C.c_void_p), ("encoder_begin_callback_user_data", C.c_void_p),
+        ("abort_callback", C.c_void_p), ("abort_callback_user_data", C.c_void_p),
+        ("logits_filter_callback", C.c_void_p), ("logits_filter_callback_user_data", C.c_void_p),
+        ("grammar_rules", C.c_void_p), ("n_grammar_rules", C.c_size_t), ("i_start_rule", C.c_size_t),
+        ("grammar_penalty", C.c_float),
+        ("vad", C.c_bool), ("vad_model_path", C.c_char_p), ("vad_params", VadParams),
+    ]
+
+
+class TokenData(C.Structure):
+    _fields_ = [("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("plog", C.c_float), ("pt", C.c_float),
+                ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64), ("t_dtw", C.c_int64), ("vlen", C.c_float)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C nobs-whisper_amd` (no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp, ip, fp = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_float)
+    sig = {
+        "whisper_context_default_params": (WhisperContextParams, []),
+        "whisper_full_default_params": (FullParams, [C.c_int]),
+        "whisper_init_from_file_with_params_no_state": (vp, [C.c_char_p, WhisperContextParams]),
+        "whisper_mi355x_init": (vp, [C.c_char_p, WhisperContextParams, C.c_int, C.c_bool]),
+        "whisper_init_state": (vp, [vp]),
+        "whisper_free": (None, [vp]),
+        "whisper_free_state": (None, [vp]),
+        "whisper_full_with_state": (C.c_int, [vp, vp, FullParams, fp, C.c_int]),
+        "whisper_full_n_segments_from_state": (C.c_int, [vp]),
+        "whisper_full_get_segment_text_from_state": (C.c_char_p, [vp, C.c_int]),
+        "whisper_full_get_segment_t0_from_state": (C.c_int64, [vp, C.c_int]),
+        "whisper_full_get_segment_t1_from_state": (C.c_int64, [vp, C.c_int]),
+        "whisper_full_n_tokens_from_state": (C.c_int, [vp, C.c_int]),
+        "whisper_full_get_token_data_from_state": (TokenData, [vp, C.c_int, C.c_int]),
+        "whisper_full_get_segment_no_speech_prob_from_state": (C.c_float, [vp, C.c_int]),
+        "whisper_full_lang_id_from_state": (C.c_int, [vp]),
+        "whisper_pcm_to_mel_with_state": (C.c_int, [vp, vp, fp, C.c_int, C.c_int]),
+        "whisper_encode_with_state": (C.c_int, [vp, vp, C.c_int, C.c_int]),
+        "whisper_decode_with_state": (C.c_int, [vp, vp, ip, C.c_int, C.c_int, C.c_int]),
+        "whisper_get_logits_from_state": (fp, [vp]),
+        "whisper_tokenize": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
+        "whisper_lang_auto_detect_with_state": (C.c_int, [vp, vp, C.c_int, C.c_int, fp]),
+        "whisper_n_vocab": (C.c_int, [vp]),
+        "whisper_token_sot": (C.c_int, [vp]),
+        "whisper_token_eot": (C.c_int, [vp]),
+        "whisper_token_beg": (C.c_int, [vp]),
+        "whisper_token_transcribe": (C.c_int, [vp]),
+        "whisper_token_to_str": (C.c_char_p, [vp, C.c_int]),
+        "whisper_lang_id": (C.c_int, [C.c_char_p]),
+        "whisper_lang_str": (C.c_char_p, [C.c_int]),
+        "whisper_mi355x_full_batch": (C.c_int, [vp, vp, FullParams, C.POINTER(vp), ip, C.c_int, C.c_bool, C.c_int]),
+        "whisper_mi355x_batch_n_segments": (C.c_int, [vp, C.c_int]),
+        "whisper_mi355x_batch_segment_text": (C.c_char_p, [vp, C.c_int, C.c_int]),
+        "whisper_mi355x_batch_segment_t0": (C.c_int64, [vp, C.c_int, C.c_int]),
+        "whisper_mi355x_batch_segment_t1": (C.c_int64, [vp, C.c_int, C.c_int]),
+        "whisper_mi355x_batch_segment_n_tokens": (C.c_int, [vp, C.c_int, C.c_int]),
+        "whisper_mi355x_batch_token_data": (TokenData, [vp, C.c_int, C.c_int, C.c_int]),
+        "whisper_mi355x_batch_lang_id": (C.c_int, [vp, C.c_int]),
+        "whisper_mi355x_batch_decoded_tokens": (C.c_long, [vp]),
+        "whisper_mi355x_phase_ms": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "whisper_mi355x_get_mel": (C.c_int, [vp, fp, C.c_int]),
+        "whisper_mi355x_get_encoder_out": (C.c_int, [vp, fp, C.c_int]),
+        "whisper_mi355x_state_stream": (vp, [vp]),
+        "whisper_mi355x_weight_arena": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "whisper_mi355x_rccl_unique_id": (C.c_int, [C.c_char_p]),
+        "whisper_mi355x_broadcast_weights": (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int]),
+        "whisper_mi355x_dev_alloc": (vp, [vp, C.c_size_t]),
+        "whisper_mi355x_dev_free": (None, [vp, vp]),
+        "whisper_mi355x_memcpy": (C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
+        "whisper_mi355x_abi_layout": (C.c_int, [C.POINTER(C.c_size_t)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+# ---- whisper-rs shaped API ---------------------------------------------------------------------
+@dataclass
+class Segment:
+    t0: int
+    t1: int
+    text: bytes
+    tokens: list
+
+
+def reference_full_params(language: str | None = "en", initial_prompt: str | None = None) -> FullParams:
+    """FullParams::new(Greedy{best_of: 1}) + the setters of src-tauri/src/whisper.rs:91-124."""
+    p = lib().whisper_full_default_params(GREEDY)
+    p.greedy.best_of = 1
+    p.language = language.encode() if language else None
+    p.initial_prompt = initial_prompt.encode() if initial_prompt else None
+    p.print_special = False
+    p.print_progress = False
+    p.print_realtime = False
+    p.print_timestamps = False
+    p.translate = False
+    p.no_context = False
+    p.single_segment = False
+    p.suppress_blank = True
+    p.no_speech_thold = 0.6
+    p.entropy_thold = 2.4
+    p.logprob_thold = -1.0
+    return p
+
+
+class WhisperContext:
+    def __init__(self, path: str, dtype: int = F16, gpu_device: int = 0, load_weights: bool = True):
+        L = lib()
+        cp = L.whisper_context_default_params()
+        cp.use_gpu = True
+        cp.gpu_device = gpu_device
+        self.L = L
+        self.ptr = L.whisper_mi355x_init(path.encode(), cp, dtype, load_weights)
+        if not self.ptr:
+            raise RuntimeError(f"whisper_mi355x_init failed for {path}")
+
+    @classmethod
+    def new_with_params(cls, path: str, use_gpu: bool = True):
+        """WhisperContext::new_with_params (whisper.rs:41-45): the plain whisper.h entry point."""
+        self = cls.__new__(cls)
+        L = lib()
+        cp = L.whisper_context_default_params()
+        cp.use_gpu = use_gpu
+        self.L = L
+        self.ptr = L.whisper_init_from_file_with_params_no_state(path.encode(), cp)
+        if not self.ptr:
+            raise RuntimeError(f"failed to load {path}")
+        return self
+
+    def create_state(self) -> "WhisperState":
+        return WhisperState(self)
+
+    def tokenize(self, text: str) -> list:
+        buf = (C.c_int * 4096)()
+        n = self.L.whisper_tokenize(self.ptr, text.encode(), buf, 4096)
+        return list(buf[:n])
+
+    def close(self):
+        if self.ptr:
+            self.L.whisper_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class WhisperState:
+    def __init__(self, ctx: WhisperContext):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.ptr = self.L.whisper_init_state(ctx.ptr)
+        if not self.ptr:
+            raise RuntimeError("whisper_init_state failed")
+
+    def full(self, params: FullParams, audio) -> int:
+        import numpy as np
+        a = np.ascontiguousarray(audio, dtype=np.float32)
+        return self.L.whisper_full_with_state(self.ctx.ptr, self.ptr, params,
+                                              a.ctypes.data_as(C.POINTER(C.c_float)), len(a))
+
+    def full_n_segments(self) -> int:
+        return self.L.whisper_full_n_segments_from_state(self.ptr)
+
+    def get_segment(self, i: int) -> Segment:
+        L = self.L
+        toks = []
+        for t in range(L.whisper_full_n_tokens_from_state(self.ptr, i)):
+            d = L.whisper_full_get_token_data_from_state(self.ptr, i, t)
+            toks.append((d.id, d.tid, d.p, d.plog))
+        return Segment(L.whisper_full_get_segment_t0_from_state(self.ptr, i),
+                       L.whisper_full_get_segment_t1_from_state(self.ptr, i),
+                       L.whisper_full_get_segment_text_from_state(self.ptr, i), toks)
+
+    def segments(self) -> list:
+        return [self.get_segment(i) for i in range(self.full_n_segments())]
+
+    def full_batch(self, params: FullParams, pcm_list, on_device: bool = False, fixed_tokens: int = 0) -> int:
+        """whisper_mi355x_full_batch. pcm_list: numpy arrays (host) or device pointers (ints)."""
+        import numpy as np
+        n = len(pcm_list)
+        ptrs = (C.c_void_p * n)()
+        lens = (C.c_int * n)()
+        keep = []
+        for i, x in enumerate(pcm_list):
+            if on_device:
+                ptrs[i], lens[i] = x[0], x[1]
+            else:
+                a = np.ascontiguousarray(x, dtype=np.float32)
+                keep.append(a)
+                ptrs[i] = a.ctypes.data
+                lens[i] = len(a)
+        return self.L.whisper_mi355x_full_batch(self.ctx.ptr, self.ptr, params, ptrs, lens, n, on_device, fixed_tokens)
+
+    def batch_segments(self, job: int) -> list:
+        L = self.L
+        out = []
+        for i in range(L.whisper_mi355x_batch_n_segments(self.ptr, job)):
+            toks = []
+            for t in range(L.whisper_mi355x_batch_segment_n_tokens(self.ptr, job, i)):
+                d = L.whisper_mi355x_batch_token_data(self.ptr, job, i, t)
+                toks.append((d.id, d.tid, d.p, d.plog))
+            out.append(Segment(L.whisper_mi355x_batch_segment_t0(self.ptr, job, i),
+                               L.whisper_mi355x_batch_segment_t1(self.ptr, job, i),
+                               L.whisper_mi355x_batch_segment_text(self.ptr, job, i), toks))
+        return out
+
+    def phase_ms(self):
+        out = (C.c_double * 5)()
+        self.L.whisper_mi355x_phase_ms(self.ptr, out)
+        return dict(zip(["mel", "encode", "prefill", "decode", "logits"], list(out)))
+
+    def close(self):
+        if self.ptr:
+            self.L.whisper_free_state(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class WhisperEngine:
+    """The C++ mirror of src-tauri/src/whisper.rs WhisperEngine (host/whisper_engine.cpp)."""
+
+    NO_MODEL = -3
+
+    def __init__(self):
+        if not os.path.exists(ENGINE_LIB_PATH):
+            raise RuntimeError(f"{ENGINE_LIB_PATH} missing: build with `make -C nobs-whisper_amd`")
+        L = C.CDLL(ENGINE_LIB_PATH)
+        L.nobs_engine_new.restype = C.c_void_p
+        L.nobs_engine_free.argtypes = [C.c_void_p]
+        L.nobs_engine_load.argtypes = [C.c_void_p, C.c_char_p]
+        L.nobs_engine_is_loaded.argtypes = [C.c_void_p]
+        L.nobs_engine_transcribe.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.c_char_p, C.c_char_p,
+                                             C.c_char_p, C.c_char_p, C.c_int]
+        self.L = L
+        self.ptr = L.nobs_engine_new()
+
+    def load_model(self, path: str) -> int:
+        return self.L.nobs_engine_load(self.ptr, path.encode())
+
+    def is_loaded(self) -> bool:
+        return bool(self.L.nobs_engine_is_loaded(self.ptr))
+
+    def transcribe(self, audio, language=None, vocabulary=None, context=None):
+        """Returns (rc, text): rc 0 ok, -1 LoadError, -2 TranscriptionError, -3 NoModel."""
+        import numpy as np
+        a = np.ascontiguousarray(audio, dtype=np.float32)
+        buf = C.create_string_buffer(1 << 20)
+        enc = lambda s: s.encode() if s is not None else None  # noqa: E731
+        rc = self.L.nobs_engine_transcribe(self.ptr, a.ctypes.data_as(C.POINTER(C.c_float)), len(a), enc(language),
+                                           enc(vocabulary), enc(context), buf, len(buf))
+        return (0, buf.value.decode("utf-8", "replace")) if rc >= 0 else (rc, None)
+
+    def __del__(self):
+        try:
+            self.L.nobs_engine_free(self.ptr)
+        except Exception:
+            pass
+
+
+def filter_hallucinations(text: str) -> str:
+    """whisper.rs:233-260 via the C++ mirror (no device needed)."""
+    L = C.CDLL(ENGINE_LIB_PATH)
+    L.nobs_filter_hallucinations.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+    buf = C.create_string_buffer(len(text.encode()) * 4 + 16)
+    n = L.nobs_filter_hallucinations(text.encode(), buf, len(buf))
+    assert n >= 0
+    return buf.value.decode()
