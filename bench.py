@@ -44,6 +44,7 @@ def load_wrs():
     import importlib.util
     spec = importlib.util.spec_from_file_location("whisper_rs", os.path.join(ROOT, "nobs-whisper_amd", "whisper_rs.py"))
     m = importlib.util.module_from_spec(spec)
+    sys.modules["whisper_rs"] = m
     spec.loader.exec_module(m)
     return m
 

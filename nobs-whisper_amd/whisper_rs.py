@@ -140,6 +140,8 @@ def lib() -> C.CDLL:
         "whisper_mi355x_dev_free": (None, [vp, vp]),
         "whisper_mi355x_memcpy": (C.c_int, [vp, vp, vp, C.c_size_t, C.c_int]),
         "whisper_mi355x_abi_layout": (C.c_int, [C.POINTER(C.c_size_t)]),
+        "whisper_mi355x_kernel_timing": (C.c_int, [vp, C.c_int]),
+        "whisper_mi355x_kernel_stats": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
