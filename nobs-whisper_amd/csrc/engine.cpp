@@ -58,7 +58,9 @@ void kt_flush(whisper_state* s) {
 }
 // GEMM launch with its algorithmic work: FLOPs for encoder-side GEMMs (MFMA-bound), HBM bytes
 // (weights + activations) for decode-side GEMMs (weight-streaming)
-static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g, hipStream_t st) {
+static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st) {
+    GemmArgs g = g0;
+    if (cls == K_GEMM_DEC) { g.splitk_ws = s->ws.splitk; g.splitk_ws_elems = s->ws.splitk_elems; }
     const double work = cls == K_GEMM_ENC ? 2.0 * g.M * g.N * g.K
                                           : 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N;
     KT kt(s, cls, work);
@@ -77,7 +79,7 @@ static void free_ws(Workspace& w) {
     // sub-allocations (pos/slot/.. of tok, win_seek/win_slot of win_job, pcm_ptrs/n_* of mel_ptrs)
     // are freed with their parent
     void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
-                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs};
+                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk};
     for (void* p : ps) dfree(p);
     if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
     if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
@@ -127,8 +129,10 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         const int L = hp.n_text_layer;
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         for (void* p : {w.cross, w.self, (void*)w.dx, w.dh, w.dq, w.datt, w.dff, w.lrow, (void*)w.logits, (void*)w.probs,
-                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs})
+                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs, (void*)w.splitk})
             dfree(p);
+        w.splitk_elems = 16L * std::min(n_tok, 256) * 4 * (long)d;
+        WM_CHECK(hipMalloc((void**)&w.splitk, w.splitk_elems * 4));
         if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
         if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
         if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));

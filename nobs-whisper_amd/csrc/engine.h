@@ -104,6 +104,8 @@ struct Workspace {
     float* dx = nullptr;
     void *dh = nullptr, *dq = nullptr, *datt = nullptr, *dff = nullptr, *lrow = nullptr;
     float *logits = nullptr, *probs = nullptr;
+    float* splitk = nullptr;  // split-K partial slabs for decode-step GEMMs
+    long splitk_elems = 0;
     int *tok = nullptr, *pos = nullptr, *slot = nullptr, *nkv_self = nullptr, *nkv_cross = nullptr, *lrows = nullptr;
     SeqCtl* ctl = nullptr;
     TokOut* tout = nullptr;

@@ -41,6 +41,8 @@ struct GemmArgs {
     float scale; int sc_div, sc_mod, sc_lim;           // column n scaled iff ((n/sc_div)%sc_mod) < sc_lim
     // caches (EPI_CROSSKV / EPI_QKV_DEC)
     void* cache; const int* row_slot; const int* row_pos; int L, layer, H, ctx, d;
+    // split-K workspace for skinny (decode-step) GEMMs: f32 [splits][M][N]; null disables split-K
+    float* splitk_ws; long splitk_ws_elems;
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);

@@ -173,19 +173,32 @@ __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, 
 #pragma unroll
         for (int e = 0; e < 8; e++) qv[e] = (float)qe[e];
     }
-    // phase 1: scores
+    // phase 1: scores; U key rows in flight per lane group before the first use
+    constexpr int U = 8;
+    const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
-    for (int t = grp; t < n_kv; t += 32) {
-        const u32x4 raw = *(const u32x4*)(K + (long)t * 64 + lane8 * 8);
-        const T* ke = (const T*)&raw;
-        float a = 0.0f;
+    for (int t0 = grp; t0 < n_kv; t0 += 32 * U) {
+        u32x4 raw[U];
 #pragma unroll
-        for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-        a += __shfl_xor(a, 1);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 4);
-        if (lane8 == 0) sc[t] = a;
-        lmax = fmaxf(lmax, a);
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 32 * u;
+            raw[u] = t < n_kv ? *(const u32x4*)(K + (long)t * 64 + lane8 * 8) : zero;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 32 * u;
+            const T* ke = (const T*)&raw[u];
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+            a += __shfl_xor(a, 1);
+            a += __shfl_xor(a, 2);
+            a += __shfl_xor(a, 4);
+            if (t < n_kv) {
+                if (lane8 == 0) sc[t] = a;
+                lmax = fmaxf(lmax, a);
+            }
+        }
     }
     // block max
     red[tid] = lmax;
@@ -215,12 +228,21 @@ __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, 
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    for (int t = grp; t < n_kv; t += 32) {
-        const u32x4 raw = *(const u32x4*)(V + (long)t * 64 + lane8 * 8);
-        const T* ve = (const T*)&raw;
-        const float p = sc[t];
+    for (int t0 = grp; t0 < n_kv; t0 += 32 * U) {
+        u32x4 raw[U];
 #pragma unroll
-        for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 32 * u;
+            raw[u] = t < n_kv ? *(const u32x4*)(V + (long)t * 64 + lane8 * 8) : zero;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 32 * u;
+            const T* ve = (const T*)&raw[u];
+            const float p = t < n_kv ? sc[t] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+        }
     }
 #pragma unroll
     for (int e = 0; e < 8; e++) acc_s[grp][lane8 * 8 + e] = acc[e];

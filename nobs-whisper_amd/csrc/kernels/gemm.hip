@@ -20,6 +20,8 @@
 #include "../common.h"
 #include "../kernels.h"
 
+#include <algorithm>
+
 namespace wm {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -60,8 +62,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
     }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int EPI>
-__global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g) {
+// SPLIT: blockIdx.z owns K range [z*kc, min(K, (z+1)*kc)) and writes its partial f32 tile to
+// g.splitk_ws[z][M][N]; splitk_reduce_kernel sums the slabs and runs the epilogue.
+template <typename T, int BM, int BN, int WM, int WN, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g, const int kc) {
     typedef typename Frag<T>::type FT;
     constexpr int BK = 64;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -102,16 +106,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g) {
         b_lds[i] = BM * 8 + row * 8 + (kc ^ ((row >> 1) & 7));
     }
 
+    const int kend = SPLIT ? min(g.K, (int)blockIdx.z * kc + kc) : g.K;
     u32x4 ra[A_PER_T], rb[B_PER_T];
     const u32x4 zero = {0, 0, 0, 0};
     auto gload = [&](int kt) {
         const int kb = kt * BK;
 #pragma unroll
         for (int i = 0; i < A_PER_T; i++)
-            ra[i] = (a_ok[i] && kb + a_k[i] < g.K) ? *(const u32x4*)(a_ptr[i] + kb) : zero;
+            ra[i] = (a_ok[i] && kb + a_k[i] < kend) ? *(const u32x4*)(a_ptr[i] + kb) : zero;
 #pragma unroll
         for (int i = 0; i < B_PER_T; i++)
-            rb[i] = (b_ok[i] && kb + b_k[i] < g.K) ? *(const u32x4*)(b_ptr[i] + kb) : zero;
+            rb[i] = (b_ok[i] && kb + b_k[i] < kend) ? *(const u32x4*)(b_ptr[i] + kb) : zero;
     };
     auto sstore = [&](int buf) {
 #pragma unroll
@@ -126,13 +131,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < TN; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (g.K + BK - 1) / BK;
-    gload(0);
+    const int k0 = SPLIT ? blockIdx.z * kc : 0;
+    const int nk = (kend - k0 + BK - 1) / BK;
+    const int kt0 = k0 / BK;
+    gload(kt0);
     sstore(0);
     __syncthreads();
     for (int kt = 0; kt < nk; kt++) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) gload(kt + 1);
+        if (kt + 1 < nk) gload(kt0 + kt + 1);
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             FT af[TM], bfr[TN];
@@ -165,20 +172,48 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+                if (m >= g.M) continue;
+                if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+                else epilogue<EPI, T>(g, m, n, acc[i][j][r]);
             }
         }
+}
+
+template <typename T, int EPI>
+__global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
+    const long total = (long)g.M * g.N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        for (int z = 0; z < splits; z++) v += g.splitk_ws[z * total + i];
+        epilogue<EPI, T>(g, (int)(i / g.N), (int)(i % g.N), v);
+    }
 }
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     if ((long)g.M * g.N >= 256L * 128 * 128) {
         dim3 grid(cdiv(g.N, 128), cdiv(g.M, 128));
-        gemm_kernel<T, 128, 128, 2, 2, EPI><<<grid, 256, 0, st>>>(g);
-    } else {
-        dim3 grid(cdiv(g.N, 64), cdiv(g.M, 64));
-        gemm_kernel<T, 64, 64, 2, 2, EPI><<<grid, 256, 0, st>>>(g);
+        gemm_kernel<T, 128, 128, 2, 2, EPI, false><<<grid, 256, 0, st>>>(g, g.K);
+        return;
     }
+    // skinny (decode-step) shapes: split K so the grid covers the 256 CUs; the weight stream is
+    // read once either way, the f32 partial slabs are M*N*splits*8 bytes of extra traffic
+    const int tiles = cdiv(g.N, 64) * cdiv(g.M, 64);
+    const int nk = cdiv(g.K, 64);
+    int splits = std::min(16, std::max(1, 512 / tiles));
+    splits = std::min(splits, std::max(1, nk / 2));
+    while (splits > 1 && (long)splits * g.M * g.N > g.splitk_ws_elems) splits--;
+    if (!g.splitk_ws || splits <= 1) {
+        dim3 grid(cdiv(g.N, 64), cdiv(g.M, 64));
+        gemm_kernel<T, 64, 64, 2, 2, EPI, false><<<grid, 256, 0, st>>>(g, g.K);
+        return;
+    }
+    const int kc = cdiv(cdiv(g.K, splits), 64) * 64;
+    splits = cdiv(g.K, kc);
+    dim3 grid(cdiv(g.N, 64), cdiv(g.M, 64), splits);
+    gemm_kernel<T, 64, 64, 2, 2, EPI, true><<<grid, 256, 0, st>>>(g, kc);
+    const long total = (long)g.M * g.N;
+    splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
 }
 
 template <typename T>

@@ -10,7 +10,9 @@
 
 namespace wm {
 
-template <typename T>
+// One wave per row; the row is loaded into registers once (NPL = ceil(D/64) floats per lane, all
+// loads issued before the first use) and reduced from registers.
+template <typename T, int NPL>
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, const int* __restrict__ rows, int M, int D,
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         T* __restrict__ y) {
@@ -19,21 +21,36 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     if (i >= M) return;
     const long r = rows ? rows[i] : i;
     const float* xr = x + r * D;
+    float v[NPL];
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        v[e] = k < D ? xr[k] : 0.0f;
+    }
     double s = 0.0;
-    for (int k = lane; k < D; k += 64) s += (double)xr[k];
+#pragma unroll
+    for (int e = 0; e < NPL; e++) s += (double)v[e];
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     const float mean = (float)(s / D);
     double s2 = 0.0;
-    for (int k = lane; k < D; k += 64) { const float v = xr[k] - mean; s2 += (double)(v * v); }
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        v[e] = v[e] - mean;
+        if (k < D) s2 += (double)(v[e] * v[e]);
+    }
     for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
     const float variance = (float)(s2 / D);
     const float scale = 1.0f / sqrtf(variance + 1e-5f);
     T* yr = y + (long)i * D;
-    for (int k = lane; k < D; k += 64) {
-        const float v = xr[k] - mean;
-        float t = v * scale;
-        t = t * w[k];
-        yr[k] = (T)(t + b[k]);
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        if (k < D) {
+            float t = v[e] * scale;
+            t = t * w[k];
+            yr[k] = (T)(t + b[k]);
+        }
     }
 }
 
@@ -48,8 +65,17 @@ __global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__
 void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b, void* y,
                       hipStream_t st) {
     if (M <= 0) return;
-    if (dt == DType::F16) layernorm_kernel<half_t><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (half_t*)y);
-    else layernorm_kernel<bf16_t><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (bf16_t*)y);
+    const int npl = cdiv(D, 64);
+#define WM_LN(N)                                                                                              \
+    if (npl <= N) {                                                                                           \
+        if (dt == DType::F16) layernorm_kernel<half_t, N><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (half_t*)y); \
+        else layernorm_kernel<bf16_t, N><<<cdiv(M, 4), 256, 0, st>>>(x, rows, M, D, w, b, (bf16_t*)y);     \
+        return;                                                                                               \
+    }
+    WM_LN(1) WM_LN(2) WM_LN(4) WM_LN(6) WM_LN(8) WM_LN(12) WM_LN(16) WM_LN(20) WM_LN(24) WM_LN(32)
+#undef WM_LN
+    fprintf(stderr, "whisper_mi355x: layernorm width %d > 2048\n", D);
+    abort();
 }
 
 void launch_embed(DType dt, const void* te, const float* pe, const int* tok, const int* pos, int n, int D, float* x,
