@@ -39,9 +39,27 @@ struct KT {
         if (!a) return;
         hipEvent_t b = kt_event(s);
         WM_CHECK(hipEventRecord(b, s->stream));
-        s->kpending.push_back({cls, a, b, work});
+        (s->capture_ev ? *s->capture_ev : s->kpending).push_back({cls, a, b, work});
     }
 };
+static void drop_graphs(whisper_state* s) {
+    for (auto& g : s->dec_graphs) {
+        hipGraphExecDestroy(g.exec);
+        for (auto& e : g.ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+    }
+    s->dec_graphs.clear();
+}
+// accumulate the timing events of one graph replay (stream already synchronised)
+static void kt_flush_graph(whisper_state* s, const whisper_state::DecGraph& g) {
+    for (auto& p : g.ev) {
+        if (!((s->ktime_mask >> p.cls) & 1)) continue;
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) continue;
+        s->kstat[p.cls].ms += ms;
+        s->kstat[p.cls].work += p.cls == K_ATTN_SELF ? s->cur_self_work : p.work;
+        s->kstat[p.cls].count++;
+    }
+}
 void kt_flush(whisper_state* s) {
     if (s->kpending.empty()) return;
     WM_CHECK(hipStreamSynchronize(s->stream));
@@ -91,6 +109,7 @@ void free_state(whisper_state* s) {
     if (!s) return;
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->stream);
+    drop_graphs(s);
     free_ws(s->ws);
     hipStreamDestroy(s->stream);
     delete s;
@@ -110,6 +129,7 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
     const size_t d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, E = esize(c->dt);
     const int n_enc = std::min(n_jobs, enc_batch_cap());
     size_t unused = 0;
+    if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
         for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job}) dfree(p);
         WM_CHECK(hipMalloc(&w.mel_img, (size_t)n_enc * 3002 * nm * E));
@@ -302,24 +322,32 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
 // n_tok tokens (ragged over slots) -> logits of n_rows rows (row r = token lrows[r]) into w.logits.
 // Token metadata must already be in w.h_ints: [tok | pos | slot | - | - ] with stride cap_tok and
 // lrows at 5*cap_tok.
-static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows) {
+// token metadata (already in w.h_ints: [tok | pos | slot | - | -], lrows at 5*cap_tok) -> device
+static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
-    const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
-    const DType dt = c->dt;
-    const Weights& W = c->w;
-    hipStream_t st = s->stream;
     int* hi = w.h_ints;
     const int ct = w.cap_tok;
-    const int KCLS = K_GEMM_DEC;
     double self_kv = 0;
     for (int i = 0; i < n_tok; i++) {
         hi[3 * ct + i] = hi[ct + i] + 1;
         hi[4 * ct + i] = hp.n_audio_ctx;
         self_kv += hi[ct + i] + 1;
     }
+    s->cur_self_work = self_kv * hp.n_text_head * 64 * 2 * 2;
+    WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, s->stream));
+}
+
+// the decoder forward over n_tok tokens + logits of n_rows rows; kernels only (graph-capturable)
+static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
+    const DType dt = c->dt;
+    const Weights& W = c->w;
+    hipStream_t st = s->stream;
+    const int KCLS = K_GEMM_DEC;
     const double kvrow = (double)H * 64 * 2 * 2;  // K and V row bytes of one position, all heads
-    WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, st));
     launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
@@ -332,7 +360,7 @@ static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows)
             tgemm(s, KCLS, dt, EPI_QKV_DEC, g, st);
         }
         {
-            KT kt(s, K_ATTN_SELF, self_kv * kvrow);
+            KT kt(s, K_ATTN_SELF, s->cur_self_work);
             launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
         }
         tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.datt, n_tok, d, Lw.wo, d, Lw.bo, w.dx, d), st);
@@ -353,6 +381,11 @@ static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows)
     }
     launch_layernorm(dt, w.dx, w.lrows, n_rows, d, W.lnd_w, W.lnd_b, w.lrow, st);
     tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+}
+
+static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows) {
+    decoder_upload(c, s, n_tok, n_rows);
+    decoder_launch(c, s, n_tok, n_rows);
 }
 
 int decode_tokens(Context* c, whisper_state* s, const int* tokens, const int* pos, const int* slots, int n_tok,
@@ -582,21 +615,26 @@ static bool process_step(Sched& S, Job& j, const TokOut& r, const float* probs_r
 }
 
 // logits kernel over the rows of `act` jobs (row r of w.logits belongs to act[r]) + D2H
-static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, std::vector<std::vector<float>>& probs_rows) {
-    Context* c = S.c;
+static bool logits_prepare(Sched& S, const std::vector<int>& act, bool want_nosp) {
     Workspace& w = S.s->ws;
-    hipStream_t st = S.s->stream;
     const int n = (int)act.size();
     bool any_probs = false;
     for (int r = 0; r < n; r++) {
         fill_ctl(S, S.jobs[act[r]], w.h_ctl[r], want_nosp);
         any_probs |= w.h_ctl[r].want_probs != 0;
     }
-    WM_CHECK(hipMemcpyAsync(w.ctl, w.h_ctl, n * sizeof(SeqCtl), hipMemcpyHostToDevice, st));
-    {
-        KT kt(S.s, K_LOGITS, (double)n * c->hp.n_vocab * 4);
-        launch_logits(w.logits, c->hp.n_vocab, w.ctl, n, c->vid, w.tout, w.probs, st);
-    }
+    WM_CHECK(hipMemcpyAsync(w.ctl, w.h_ctl, n * sizeof(SeqCtl), hipMemcpyHostToDevice, S.s->stream));
+    return any_probs;
+}
+static void logits_launch(Context* c, whisper_state* s, int n) {
+    Workspace& w = s->ws;
+    KT kt(s, K_LOGITS, (double)n * c->hp.n_vocab * 4);
+    launch_logits(w.logits, c->hp.n_vocab, w.ctl, n, c->vid, w.tout, w.probs, s->stream);
+}
+static void logits_finish(Sched& S, int n, bool any_probs, std::vector<std::vector<float>>& probs_rows) {
+    Context* c = S.c;
+    Workspace& w = S.s->ws;
+    hipStream_t st = S.s->stream;
     WM_CHECK(hipMemcpyAsync(w.h_tout, w.tout, n * sizeof(TokOut), hipMemcpyDeviceToHost, st));
     probs_rows.assign(n, {});
     if (any_probs) {  // sampling clips (t > 0): probs and logprobs rows for std::discrete_distribution
@@ -608,6 +646,52 @@ static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, st
             }
     }
     WM_CHECK(hipStreamSynchronize(st));
+}
+static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, std::vector<std::vector<float>>& probs_rows) {
+    const bool any = logits_prepare(S, act, want_nosp);
+    logits_launch(S.c, S.s, (int)act.size());
+    logits_finish(S, (int)act.size(), any, probs_rows);
+}
+
+static bool use_graphs() {
+    const char* e = getenv("WHISPER_MI355X_GRAPH");
+    return !(e && e[0] == '0');
+}
+
+// One decode step (decoder over n active clips + logits kernel) as a replayed hipGraph: the host
+// cost of ~11 launches per layer is paid once per distinct n at capture time.
+static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::vector<float>>& probs_rows) {
+    Context* c = S.c;
+    whisper_state* s = S.s;
+    const int n = (int)act.size();
+    decoder_upload(c, s, n, n);
+    const bool any = logits_prepare(S, act, false);
+    if (!use_graphs()) {
+        decoder_launch(c, s, n, n);
+        logits_launch(c, s, n);
+        logits_finish(S, n, any, probs_rows);
+        return;
+    }
+    whisper_state::DecGraph* G = nullptr;
+    for (auto& g : s->dec_graphs)
+        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask) G = &g;
+    if (!G) {
+        whisper_state::DecGraph g{n, n, s->ktime_mask, nullptr, {}};
+        hipGraph_t graph;
+        s->capture_ev = &g.ev;
+        WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        decoder_launch(c, s, n, n);
+        logits_launch(c, s, n);
+        WM_CHECK(hipStreamEndCapture(s->stream, &graph));
+        s->capture_ev = nullptr;
+        WM_CHECK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+        WM_CHECK(hipGraphDestroy(graph));
+        s->dec_graphs.push_back(std::move(g));
+        G = &s->dec_graphs.back();
+    }
+    WM_CHECK(hipGraphLaunch(G->exec, s->stream));
+    logits_finish(S, n, any, probs_rows);
+    kt_flush_graph(s, *G);
 }
 
 int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
@@ -803,8 +887,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
                     hi[2 * w.cap_tok + r] = j.slot;
                     hi[5 * w.cap_tok + r] = r;
                 }
-                decoder_forward(c, s, na, na);
-                run_logits(S, act, false, probs_rows);
+                decode_step(S, act, probs_rows);
                 S.t_decode += now_ms() - td;
                 for (int r = 0; r < na; r++) {
                     Job& j = S.jobs[act[r]];

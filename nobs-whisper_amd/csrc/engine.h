@@ -153,6 +153,11 @@ struct whisper_state {
     struct KPending { int cls; hipEvent_t a, b; double work; };
     std::vector<KPending> kpending;
     std::vector<hipEvent_t> kpool;
+    // decode steps replayed as hipGraphs (one per active-sequence count and timing mask)
+    struct DecGraph { int n_tok, n_rows, mask; hipGraphExec_t exec; std::vector<KPending> ev; };
+    std::vector<DecGraph> dec_graphs;
+    std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
+    double cur_self_work = 0;                     // self-attention bytes of the current step
 };
 
 struct whisper_context {
