@@ -69,6 +69,13 @@ WHISPER_API int whisper_mi355x_get_encoder_out(struct whisper_state * state, flo
 WHISPER_API int whisper_mi355x_kernel_timing(struct whisper_state * state, int class_mask);
 WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cls, double out[3]);
 
+/* Kernel-level test/tuning hooks (device pointers): one fused-epilogue GEMM launch of the engine
+ * (epi as in kernels.h: 0 store, 1 gelu, 2 residual f32, 4 f32), averaged over reps; and the
+ * GEMM variant override (-1 auto, 0 register-staged, 1 LDS-DMA). */
+WHISPER_API int whisper_mi355x_debug_gemm(struct whisper_context * ctx, int epi, const void * A, int M, int K,
+                                          const void * B, int N, const float * bias, void * out, int reps, float * ms);
+WHISPER_API void whisper_mi355x_set_gemm_variant(int variant);
+
 /* ABI self-description, no device needed: sizeof(whisper_full_params), sizeof(whisper_context_params),
  * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /
  * new_segment_callback / vad_params). Lets a binding (bindgen, ctypes) be checked field-by-field. */

@@ -10,6 +10,7 @@
 #include "../../include/whisper_mi355x.h"
 #include "engine.h"
 
+namespace wm { extern int g_gemm_variant; }
 using namespace wm;
 
 static Context* C(whisper_context* ctx) { return ctx ? &ctx->c : nullptr; }
@@ -466,6 +467,38 @@ int whisper_mi355x_kernel_stats(struct whisper_state* s, int cls, double out[3])
     out[0] = s->kstat[cls].ms;
     out[1] = (double)s->kstat[cls].count;
     out[2] = s->kstat[cls].work;
+    return 0;
+}
+// ---- kernel-level test/tuning hooks ---------------------------------------------------------------
+
+void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
+// out[M][N] (f32 for epi EPI_F32 / EPI_RESID, else the context dtype) = A[M][K] . B[N][K]^T + bias,
+// all device pointers; runs `reps` times and returns the average ms per launch in *ms.
+int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B, int N,
+                              const float* bias, void* out, int reps, float* ms) {
+    if (!ctx) return -1;
+    hipSetDevice(ctx->c.device);
+    hipStream_t st;
+    WM_CHECK(hipStreamCreate(&st));
+    GemmArgs g{};
+    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+    g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    hipEvent_t e0, e1;
+    WM_CHECK(hipEventCreate(&e0));
+    WM_CHECK(hipEventCreate(&e1));
+    launch_gemm(ctx->c.dt, epi, g, st);  // warm
+    WM_CHECK(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++) launch_gemm(ctx->c.dt, epi, g, st);
+    WM_CHECK(hipEventRecord(e1, st));
+    WM_CHECK(hipStreamSynchronize(st));
+    float t = 0;
+    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+    if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipStreamDestroy(st);
     return 0;
 }
 // ABI self-description (no device needed): sizes/offsets that a binding generator must agree on.

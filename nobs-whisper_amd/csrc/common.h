@@ -55,6 +55,46 @@ __device__ __forceinline__ float gelu_ggml(float x) {
     return (float)(half_t)g;
 }
 
+// Block-wide (256-thread) LayerNorm of one row held in registers: thread t owns columns
+// t + 256*k. ggml_norm arithmetic: double sums, float mean/variance, 1/sqrtf(var + 1e-5), then
+// (v*scale)*w + b with every op separately rounded (explicit _rn intrinsics: no FMA contraction
+// whatever the file's -ffp-contract). `sh` is >= 4 doubles of LDS.
+__device__ __forceinline__ double block256_sum_d(double x, double* sh) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[w] = x;
+    __syncthreads();
+    const double r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+    __syncthreads();
+    return r;
+}
+template <typename T, int NPT>
+__device__ __forceinline__ void block256_layernorm(float (&v)[NPT], int D, const float* __restrict__ w,
+                                                   const float* __restrict__ b, T* __restrict__ y, double* sh) {
+    const int tid = threadIdx.x;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; k++)
+        if (tid + 256 * k < D) s += (double)v[k];
+    s = block256_sum_d(s, sh);
+    const float mean = (float)(s / D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; k++)
+        if (tid + 256 * k < D) {
+            v[k] = __fsub_rn(v[k], mean);
+            s2 += (double)__fmul_rn(v[k], v[k]);
+        }
+    s2 = block256_sum_d(s2, sh);
+    const float variance = (float)(s2 / D);
+    const float scale = 1.0f / sqrtf(variance + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int n = tid + 256 * k;
+        if (n < D) y[n] = (T)__fadd_rn(__fmul_rn(__fmul_rn(v[k], scale), w[n]), b[n]);
+    }
+}
+
 // host-side conversions (weights are converted once at load)
 static inline float h2f(uint16_t h) {
     const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;

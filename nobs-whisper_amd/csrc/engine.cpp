@@ -338,8 +338,10 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) 
     WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, s->stream));
 }
 
-// the decoder forward over n_tok tokens + logits of n_rows rows; kernels only (graph-capturable)
-static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows) {
+// the decoder forward over n_tok tokens + logits of n_rows rows; kernels only (graph-capturable).
+// Decode steps (one token per clip, logits for every row, <= 128 rows) take the fused path: every
+// LayerNorm is folded into the embedding or into the split-K reduce of the preceding residual GEMM.
+static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
     const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
@@ -348,10 +350,20 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows) 
     hipStream_t st = s->stream;
     const int KCLS = K_GEMM_DEC;
     const double kvrow = (double)H * 64 * 2 * 2;  // K and V row bytes of one position, all heads
-    launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
+    const bool fused = rows_identity && n_rows == n_tok && n_tok <= 128;
+    auto resid = [&](const void* A, int K, const void* Wt, const float* bias, const float* lnw, const float* lnb) {
+        GemmArgs g = gemm_plain(A, n_tok, K, Wt, d, bias, w.dx, d);
+        if (fused) { g.ln_w = lnw; g.ln_b = lnb; g.ln_out = w.dh; }
+        tgemm(s, KCLS, dt, EPI_RESID, g, st);
+        if (!fused && lnw) launch_layernorm(dt, w.dx, nullptr, n_tok, d, lnw, lnb, w.dh, st);
+    };
+    if (fused) launch_embed_ln(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, W.dec[0].ln1_w, W.dec[0].ln1_b, w.dh, st);
+    else {
+        launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
+        launch_layernorm(dt, w.dx, nullptr, n_tok, d, W.dec[0].ln1_w, W.dec[0].ln1_b, w.dh, st);
+    }
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
-        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.ln1_w, Lw.ln1_b, w.dh, st);
         {
             GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wqkv, 3 * d, Lw.bqkv, w.dq, d);
             g.scale = c->k_scale;
@@ -363,8 +375,7 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows) 
             KT kt(s, K_ATTN_SELF, s->cur_self_work);
             launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
         }
-        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.datt, n_tok, d, Lw.wo, d, Lw.bo, w.dx, d), st);
-        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.lnx_w, Lw.lnx_b, w.dh, st);
+        resid(w.datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
         {
             GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
@@ -374,18 +385,23 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows) 
             KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);
             launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
         }
-        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.datt, n_tok, d, Lw.wxo, d, Lw.bxo, w.dx, d), st);
-        launch_layernorm(dt, w.dx, nullptr, n_tok, d, Lw.ln2_w, Lw.ln2_b, w.dh, st);
+        resid(w.datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
         tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, w.dff, 4 * d), st);
-        tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.dff, n_tok, 4 * d, Lw.w2, d, Lw.b2, w.dx, d), st);
+        if (l + 1 < L) resid(w.dff, 4 * d, Lw.w2, Lw.b2, W.dec[l + 1].ln1_w, W.dec[l + 1].ln1_b);
+        else if (fused) resid(w.dff, 4 * d, Lw.w2, Lw.b2, W.lnd_w, W.lnd_b);  // dh = final LN of every row
+        else resid(w.dff, 4 * d, Lw.w2, Lw.b2, nullptr, nullptr);
     }
-    launch_layernorm(dt, w.dx, w.lrows, n_rows, d, W.lnd_w, W.lnd_b, w.lrow, st);
-    tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+    if (fused) {
+        tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.dh, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+    } else {
+        launch_layernorm(dt, w.dx, w.lrows, n_rows, d, W.lnd_w, W.lnd_b, w.lrow, st);
+        tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+    }
 }
 
-static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows) {
+static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity = false) {
     decoder_upload(c, s, n_tok, n_rows);
-    decoder_launch(c, s, n_tok, n_rows);
+    decoder_launch(c, s, n_tok, n_rows, rows_identity);
 }
 
 int decode_tokens(Context* c, whisper_state* s, const int* tokens, const int* pos, const int* slots, int n_tok,
@@ -592,7 +608,12 @@ static bool process_step(Sched& S, Job& j, const TokOut& r, const float* probs_r
         j.has_ts = true;
     }
     if (S.o.fixed_tokens > 0) {
-        if (i == S.n_max_steps - 1) { j.result_len = S.n_max_steps; j.completed = true; return false; }
+        if (i == S.n_max_steps - 1) {  // fixed-work mode: one full window per chunk
+            j.result_len = S.n_max_steps;
+            j.seek_delta = 100 * WHISPER_CHUNK_SIZE;
+            j.completed = true;
+            return false;
+        }
     } else if (td.id == v.token_eot || (p.max_tokens > 0 && i >= p.max_tokens) ||
                (j.has_ts && j.seek + j.seek_delta + delta_min >= j.seek_end)) {
         if (j.result_len == 0 && !p.no_timestamps) {
@@ -667,7 +688,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     decoder_upload(c, s, n, n);
     const bool any = logits_prepare(S, act, false);
     if (!use_graphs()) {
-        decoder_launch(c, s, n, n);
+        decoder_launch(c, s, n, n, true);
         logits_launch(c, s, n);
         logits_finish(S, n, any, probs_rows);
         return;
@@ -680,7 +701,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        decoder_launch(c, s, n, n);
+        decoder_launch(c, s, n, n, true);
         logits_launch(c, s, n);
         WM_CHECK(hipStreamEndCapture(s->stream, &graph));
         s->capture_ev = nullptr;

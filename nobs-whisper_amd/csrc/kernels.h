@@ -19,6 +19,9 @@ void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, c
 // x[i][:] = tok_emb[tok[i]][:] + pos_emb[pos[i]][:]   (f32 out)
 void launch_embed(DType dt, const void* tok_emb, const float* pos_emb, const int* tok, const int* pos, int n, int D,
                   float* x, hipStream_t st);
+// embedding fused with the first LayerNorm: x as above, y[i] = LN(x[i]) * w + b (T out)
+void launch_embed_ln(DType dt, const void* tok_emb, const float* pos_emb, const int* tok, const int* pos, int n, int D,
+                     float* x, const float* w, const float* b, void* y, hipStream_t st);
 
 // ---- GEMM (kernels/gemm.hip): C[M][N] = A[M][K] . B[N][K]^T + bias, fused epilogues --------------
 enum Epi : int {
@@ -43,6 +46,9 @@ struct GemmArgs {
     void* cache; const int* row_slot; const int* row_pos; int L, layer, H, ctx, d;
     // split-K workspace for skinny (decode-step) GEMMs: f32 [splits][M][N]; null disables split-K
     float* splitk_ws; long splitk_ws_elems;
+    // EPI_RESID on the split-K path only: fused LayerNorm of the updated residual rows,
+    // ln_out[m][:] = LN(out[m][:]) * ln_w + ln_b (the next GEMM's input; null = no LN)
+    const float* ln_w; const float* ln_b; void* ln_out;
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);

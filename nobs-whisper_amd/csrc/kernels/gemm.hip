@@ -179,6 +179,100 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs g, const int k
         }
 }
 
+// Large-M (encoder / cross-KV / prefill) GEMM: 128x128x64 tiles staged global->LDS by
+// global_load_lds_dwordx4 (no register staging), two LDS stages, 4 waves x (64x64) of
+// v_mfma_f32_16x16x32. The LDS image is the same XOR-swizzled [row][8 x 16 B] image as above: the
+// DMA writes lane-linearly (wave base + lane*16), so the swizzle is applied to the per-lane
+// SOURCE address (lane l of an 8-row piece loads logical chunk (l&7)^((row>>1)&7)), and the
+// fragment reads apply the same involution. Rows past M/N are clamped to the last valid row
+// (their outputs are never stored); K must be a multiple of 64. Blocks are remapped so that the
+// tiles sharing an A row-panel run on the same XCD (bijective remap, guide T1).
+template <typename T, int EPI>
+__global__ void __launch_bounds__(256) gemm_glds_kernel(const GemmArgs g, const int tiles_n) {
+    typedef typename Frag<T>::type FT;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int BM = 128, BN = 128, BK = 64;
+    __shared__ u32x4 lds[2][(BM + BN) * 8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int m0 = (wgid / tiles_n) * BM, n0 = (wgid % tiles_n) * BN;
+    const T* A = (const T*)g.A;
+    const T* B = (const T*)g.B;
+    const T* a_src[4];
+    const T* b_src[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int m = min(m0 + r, g.M - 1);
+        a_src[i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 8;
+        const int n = min(n0 + r, g.N - 1);
+        b_src[i] = B + (long)n * g.K + c * 8;
+    }
+    auto issue = [&](int stage, int kt) {
+        const int kb = kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + kb), (lds_ptr_t)&lds[stage][(wave * 4 + i) * 64], 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + kb), (lds_ptr_t)&lds[stage][BM * 8 + (wave * 4 + i) * 64],
+                                             16, 0, 0);
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nk = g.K / BK;
+    issue(0, 0);
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+            issue(cur ^ 1, kt + 1);
+            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            FT af[4], bfr[4];
+            const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = wm * 64 + i * 16 + (lane & 15);
+                af[i] = __builtin_bit_cast(FT, lds[cur][row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = wn * 64 + j * 16 + (lane & 15);
+                bfr[j] = __builtin_bit_cast(FT, lds[cur][BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (n >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+            }
+        }
+}
+
+int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA
+
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
     const long total = (long)g.M * g.N;
@@ -189,17 +283,76 @@ __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
     }
 }
 
+// split-K reduce of a residual GEMM fused with the next LayerNorm: one block per row m; the
+// updated residual row stays in registers for the LN (decode steps: saves a launch per LN).
+template <typename T, int NPT>
+__global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmArgs g, int splits) {
+    __shared__ double sh[4];
+    const int m = blockIdx.x, tid = threadIdx.x;
+    const long total = (long)g.M * g.N;
+    float* xrow = (float*)g.out + (long)m * g.ldo;
+    float v[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int n = tid + 256 * k;
+        v[k] = 0.0f;
+        if (n < g.N) {
+            float a = 0.0f;
+            for (int z = 0; z < splits; z++) a += g.splitk_ws[z * total + (long)m * g.N + n];
+            if (g.bias) a = a + g.bias[n];
+            const float x = a + xrow[n];
+            xrow[n] = x;
+            v[k] = x;
+        }
+    }
+    block256_layernorm<T, NPT>(v, g.N, g.ln_w, g.ln_b, (T*)g.ln_out + (long)m * g.N, sh);
+}
+
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
+    if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
+        const int tn = cdiv(g.N, 128);
+        gemm_glds_kernel<T, EPI><<<tn * cdiv(g.M, 128), 256, 0, st>>>(g, tn);
+        return;
+    }
     if ((long)g.M * g.N >= 256L * 128 * 128) {
         dim3 grid(cdiv(g.N, 128), cdiv(g.M, 128));
         gemm_kernel<T, 128, 128, 2, 2, EPI, false><<<grid, 256, 0, st>>>(g, g.K);
         return;
     }
-    // skinny (decode-step) shapes: split K so the grid covers the 256 CUs; the weight stream is
-    // read once either way, the f32 partial slabs are M*N*splits*8 bytes of extra traffic
-    const int tiles = cdiv(g.N, 64) * cdiv(g.M, 64);
+    const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
     const int nk = cdiv(g.K, 64);
+    if (g.splitk_ws && g.M <= 128) {
+        // decode step (M = active clips <= 128): one M tile, the weight stream read exactly once;
+        // K split to ~128 workgroups with >= 4 K-tiles each (partial slabs: M*N*splits*8 bytes)
+        const int BM = g.M <= 64 ? 64 : 128;
+        const int tiles = cdiv(g.N, 64);
+        int splits = std::min(std::max(1, 128 / tiles), std::max(1, nk / 4));
+        while (splits > 1 && (long)splits * g.M * g.N > g.splitk_ws_elems) splits--;
+        if (splits > 1 || fused_ln) {
+            const int kc = cdiv(cdiv(g.K, splits), 64) * 64;
+            splits = cdiv(g.K, kc);
+            dim3 grid(tiles, 1, splits);
+            if (BM == 64) gemm_kernel<T, 64, 64, 2, 2, EPI, true><<<grid, 256, 0, st>>>(g, kc);
+            else gemm_kernel<T, 128, 64, 2, 2, EPI, true><<<grid, 256, 0, st>>>(g, kc);
+            if (fused_ln) {
+                const int npt = cdiv(g.N, 256);
+                if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
+                else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
+                else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+            } else {
+                const long total = (long)g.M * g.N;
+                splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
+            }
+        } else {
+            dim3 grid(tiles, 1);
+            if (BM == 64) gemm_kernel<T, 64, 64, 2, 2, EPI, false><<<grid, 256, 0, st>>>(g, g.K);
+            else gemm_kernel<T, 128, 64, 2, 2, EPI, false><<<grid, 256, 0, st>>>(g, g.K);
+        }
+        return;
+    }
+    if (fused_ln) { fprintf(stderr, "whisper_mi355x: fused LN requires the decode split-K path\n"); abort(); }
+    const int tiles = cdiv(g.N, 64) * cdiv(g.M, 64);
     int splits = std::min(16, std::max(1, 512 / tiles));
     splits = std::min(splits, std::max(1, nk / 2));
     while (splits > 1 && (long)splits * g.M * g.N > g.splitk_ws_elems) splits--;

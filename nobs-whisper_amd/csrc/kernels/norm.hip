@@ -62,6 +62,41 @@ __global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__
     for (int k = threadIdx.x; k < D; k += blockDim.x) x[(long)i * D + k] = (float)te[t * D + k] + pe[p * D + k];
 }
 
+// decoder token + position embedding fused with the first layer's LayerNorm (one block per token)
+template <typename T, int NPT>
+__global__ void __launch_bounds__(256) embed_ln_kernel(const T* __restrict__ te, const float* __restrict__ pe,
+                                                       const int* __restrict__ tok, const int* __restrict__ pos, int D,
+                                                       float* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ b, T* __restrict__ y) {
+    __shared__ double sh[4];
+    const int i = blockIdx.x;
+    const long t = tok[i], p = pos[i];
+    float v[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int n = threadIdx.x + 256 * k;
+        v[k] = 0.0f;
+        if (n < D) {
+            v[k] = (float)te[t * D + n] + pe[p * D + n];
+            x[(long)i * D + n] = v[k];
+        }
+    }
+    block256_layernorm<T, NPT>(v, D, w, b, y + (long)i * D, sh);
+}
+
+void launch_embed_ln(DType dt, const void* te, const float* pe, const int* tok, const int* pos, int n, int D, float* x,
+                     const float* w, const float* b, void* y, hipStream_t st) {
+    if (n <= 0) return;
+    if (D > 2048) { fprintf(stderr, "whisper_mi355x: embed LN width %d > 2048\n", D); abort(); }
+    if (D <= 1024) {
+        if (dt == DType::F16) embed_ln_kernel<half_t, 4><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x, w, b, (half_t*)y);
+        else embed_ln_kernel<bf16_t, 4><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x, w, b, (bf16_t*)y);
+    } else {
+        if (dt == DType::F16) embed_ln_kernel<half_t, 8><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x, w, b, (half_t*)y);
+        else embed_ln_kernel<bf16_t, 8><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x, w, b, (bf16_t*)y);
+    }
+}
+
 void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b, void* y,
                       hipStream_t st) {
     if (M <= 0) return;

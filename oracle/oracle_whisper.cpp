@@ -756,7 +756,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
                         dec.has_ts = true;
                     }
                     if (p.fixed_tokens > 0) {
-                        if (i == n_steps - 1) { dec.sequence.result_len = n_steps; dec.completed = true; break; }
+                        if (i == n_steps - 1) { dec.sequence.result_len = n_steps; dec.seek_delta = 3000; dec.completed = true; break; }
                     } else if (tok.id == vocab.token_eot || (p.max_tokens > 0 && i >= p.max_tokens) ||
                                (dec.has_ts && seek + dec.seek_delta + delta_min >= seek_end)) {
                         if (dec.sequence.result_len == 0 && !p.no_timestamps) {

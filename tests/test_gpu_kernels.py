@@ -1,0 +1,61 @@
+"""Kernel-level GPU parity: the MFMA GEMM (both staging variants, split-K path) against a float64
+numpy reference of the same f16 operands. Tolerance: |err| <= 1e-4 * sum_k |a_k b_k| + 1e-5 (f32
+accumulation of f16-exact products; order differs from numpy)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(wrs, micro_model):
+    c = wrs.WhisperContext(micro_model, dtype=wrs.F16)
+    yield c
+    c.close()
+
+
+def _dev(wrs, ctx, arr):
+    L = wrs.lib()
+    p = L.whisper_mi355x_dev_alloc(ctx.ptr, arr.nbytes)
+    assert p
+    L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(p), arr.ctypes.data, arr.nbytes, 1)
+    return p
+
+
+def _run_gemm(wrs, ctx, A, B, bias, variant, reps=1):
+    L = wrs.lib()
+    L.whisper_mi355x_debug_gemm.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                            C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_float)]
+    L.whisper_mi355x_set_gemm_variant.argtypes = [C.c_int]
+    M, K = A.shape
+    N = B.shape[0]
+    pa, pb, pbias = _dev(wrs, ctx, A), _dev(wrs, ctx, B), _dev(wrs, ctx, bias)
+    out = np.zeros((M, N), np.float32)
+    po = _dev(wrs, ctx, out)
+    L.whisper_mi355x_set_gemm_variant(variant)
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_gemm(ctx.ptr, 4, C.c_void_p(pa), M, K, C.c_void_p(pb), N, C.c_void_p(pbias),
+                                       C.c_void_p(po), reps, C.byref(ms)) == 0
+    L.whisper_mi355x_set_gemm_variant(-1)
+    L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(po), out.nbytes, 2)
+    for p in (pa, pb, pbias, po):
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    return out, ms.value
+
+
+@pytest.mark.parametrize("M,N,K", [(1500 * 2 + 5, 1280, 1280), (3000, 51866, 384), (257, 384, 1536),
+                                   (32, 1280, 5120), (128, 3840, 1280), (7, 51866, 384)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gemm_matches_numpy(wrs, ctx, M, N, K, variant):
+    rng = np.random.default_rng(M * 7 + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float16)
+    B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    out, _ = _run_gemm(wrs, ctx, A, B, bias, variant)
+    A64, B64 = A.astype(np.float64), B.astype(np.float64)
+    ref = A64 @ B64.T + bias
+    bound = 1e-4 * (np.abs(A64) @ np.abs(B64).T) + 1e-5
+    err = np.abs(out - ref)
+    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
