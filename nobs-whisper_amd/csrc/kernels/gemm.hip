@@ -271,7 +271,97 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const GemmArgs g, const 
         }
 }
 
-int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA
+// 256x256x64 tiles, 8 waves (2 x 4), each wave 128x64 (8 x 4 MFMA 16x16x32 tiles, 128 accumulator
+// registers): twice the MFMA work per barrier of the 128x128 kernel and 0.375 LDS fragment reads
+// per MFMA. Same LDS-DMA staging, swizzle and XCD remap; 2 stages x 64 KiB LDS, one block per CU.
+template <typename T, int EPI>
+__global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const int tiles_n) {
+    typedef typename Frag<T>::type FT;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int BM = 256, BN = 256, BK = 64;
+    __shared__ u32x4 lds[2][(BM + BN) * 8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int m0 = (wgid / tiles_n) * BM, n0 = (wgid % tiles_n) * BN;
+    const T* A = (const T*)g.A;
+    const T* B = (const T*)g.B;
+    // A tile = 32 pieces of 8 rows x 128 B; 8 waves x 4 pieces. Same for B.
+    const T* a_src[4];
+    const T* b_src[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int m = min(m0 + r, g.M - 1);
+        a_src[i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 8;
+        const int n = min(n0 + r, g.N - 1);
+        b_src[i] = B + (long)n * g.K + c * 8;
+    }
+    auto issue = [&](int stage, int kt) {
+        const int kb = kt * BK;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + kb), (lds_ptr_t)&lds[stage][(wave * 4 + i) * 64], 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + kb), (lds_ptr_t)&lds[stage][BM * 8 + (wave * 4 + i) * 64],
+                                             16, 0, 0);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nk = g.K / BK;
+    issue(0, 0);
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+            issue(cur ^ 1, kt + 1);
+            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            FT af[8], bfr[4];
+            const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = wn * 64 + j * 16 + (lane & 15);
+                bfr[j] = __builtin_bit_cast(FT, lds[cur][BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int row = wm * 128 + i * 16 + (lane & 15);
+                af[i] = __builtin_bit_cast(FT, lds[cur][row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (n >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+            }
+        }
+}
+
+int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2
 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
@@ -310,6 +400,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
+    if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant == 2) {
+        const int tn = cdiv(g.N, 256);
+        gemm256_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        return;
+    }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
         const int tn = cdiv(g.N, 128);
         gemm_glds_kernel<T, EPI><<<tn * cdiv(g.M, 128), 256, 0, st>>>(g, tn);
