@@ -62,6 +62,84 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
     }
 }
 
+// 16 consecutive outputs of row m starting at column n (n % 16 == 0): the same math as
+// `epilogue`, with 16-byte loads/stores whenever the row segment is in bounds and aligned.
+template <int EPI, typename T>
+__device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, float (&v)[16]) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    bool vec = n + 16 <= g.N && EPI != EPI_QKV_DEC;
+    long base = 0;
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
+        base = orow * g.ldo + n;
+        vec = vec && (((uintptr_t)((T*)g.out + base)) & 15) == 0;
+    } else if constexpr (EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_GELU_POS) {
+        base = (long)m * g.ldo + n;
+        vec = vec && (((uintptr_t)((float*)g.out + base)) & 15) == 0;
+    }
+    if (!vec) {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (n + k < g.N) epilogue<EPI, T>(g, m, n + k, v[k]);
+        return;
+    }
+    if (g.bias) {
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            const float4 b = *(const float4*)(g.bias + n + k);
+            v[k] = v[k] + b.x; v[k + 1] = v[k + 1] + b.y; v[k + 2] = v[k + 2] + b.z; v[k + 3] = v[k + 3] + b.w;
+        }
+    }
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_CROSSKV) {
+        float sc = 1.0f;
+        T* dst;
+        if constexpr (EPI == EPI_CROSSKV) {
+            const int b = m / g.ctx, t = m % g.ctx;
+            const int l = n / (2 * g.d), kv = (n / g.d) & 1, h = (n % g.d) >> 6, dh = n & 63;
+            if (kv == 0) sc = g.scale;
+            const long slot = g.row_slot[b];
+            dst = (T*)g.cache + ((((slot * g.L + l) * 2 + kv) * g.H + h) * g.ctx + t) * 64 + dh;
+        } else {
+            if constexpr (EPI == EPI_STORE)
+                if (g.sc_div > 0 && ((n / g.sc_div) % g.sc_mod) < g.sc_lim) sc = g.scale;
+            dst = (T*)g.out + base;
+        }
+        T o[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            float x = v[k];
+            if constexpr (EPI == EPI_GELU) x = gelu_ggml(x);
+            else if (sc != 1.0f) x = x * sc;
+            o[k] = (T)x;
+        }
+        *(u4*)dst = *(const u4*)&o[0];
+        *(u4*)(dst + 8) = *(const u4*)&o[8];
+    } else if constexpr (EPI == EPI_RESID) {
+        float* o = (float*)g.out + base;
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            float4 x = *(const float4*)(o + k);
+            x.x = v[k] + x.x; x.y = v[k + 1] + x.y; x.z = v[k + 2] + x.z; x.w = v[k + 3] + x.w;
+            *(float4*)(o + k) = x;
+        }
+    } else if constexpr (EPI == EPI_GELU_POS) {
+        float* o = (float*)g.out + base;
+        const float* p = g.pos + (long)(m % g.pos_rows) * g.N + n;
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            const float4 pp = *(const float4*)(p + k);
+            float4 x;
+            x.x = gelu_ggml(v[k]) + pp.x; x.y = gelu_ggml(v[k + 1]) + pp.y;
+            x.z = gelu_ggml(v[k + 2]) + pp.z; x.w = gelu_ggml(v[k + 3]) + pp.w;
+            *(float4*)(o + k) = x;
+        }
+    } else if constexpr (EPI == EPI_F32) {
+        float* o = (float*)g.out + base;
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) *(float4*)(o + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+    }
+}
+
 // SPLIT: blockIdx.z owns K range [z*kc, min(K, (z+1)*kc)) and writes its partial f32 tile to
 // g.splitk_ws[z][M][N]; splitk_reduce_kernel sums the slabs and runs the epilogue.
 template <typename T, int BM, int BN, int WM, int WN, int EPI, bool SPLIT>
@@ -347,18 +425,30 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    // epilogue: each wave transposes its 128x64 tile through LDS 16 rows at a time so every lane
+    // owns 16 consecutive columns of one row (16-byte stores instead of 4-byte column stores)
+    constexpr int LDW = 68;  // padded f32 row stride of the staging image
+    float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
 #pragma unroll
-    for (int i = 0; i < 8; i++)
+    for (int i = 0; i < 8; i++) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-            if (n >= g.N) continue;
+        for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int m = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
-            }
+            for (int r = 0; r < 4; r++) stg[((lane >> 4) * 4 + r) * LDW + j * 16 + (lane & 15)] = acc[i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int row = lane >> 2, c0 = (lane & 3) * 16;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            const float4 x = *(const float4*)(stg + row * LDW + c0 + k);
+            v[k] = x.x; v[k + 1] = x.y; v[k + 2] = x.z; v[k + 3] = x.w;
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if (m < g.M && n < g.N) epilogue16<EPI, T>(g, m, n, v);
+    }
 }
 
 int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2
@@ -400,7 +490,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
-    if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant == 2) {
+    const bool big256 = g_gemm_variant == 2 || (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
+    if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && big256) {
         const int tn = cdiv(g.N, 256);
         gemm256_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         return;
