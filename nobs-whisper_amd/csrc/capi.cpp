@@ -485,6 +485,10 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
     g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
     g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
     g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    if (M <= 128) {  // decode-step shapes take the split-K path, as in the engine
+        g.splitk_ws_elems = 64L * M * N;
+        WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+    }
     hipEvent_t e0, e1;
     WM_CHECK(hipEventCreate(&e0));
     WM_CHECK(hipEventCreate(&e1));
@@ -499,6 +503,7 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     hipStreamDestroy(st);
+    if (g.splitk_ws) hipFree(g.splitk_ws);
     return 0;
 }
 // ABI self-description (no device needed): sizes/offsets that a binding generator must agree on.

@@ -40,6 +40,13 @@ __device__ __forceinline__ f32x4 mfma16x16x32(half8 a, half8 b, f32x4 c) {
 __device__ __forceinline__ f32x4 mfma16x16x32(bfx8 a, bfx8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32x32x16(half8 a, half8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32x32x16(bfx8 a, bfx8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 
 template <typename T> __device__ __forceinline__ T to_t(float x) { return (T)x; }
 template <typename T> __device__ __forceinline__ float from_t(T x) { return (float)x; }

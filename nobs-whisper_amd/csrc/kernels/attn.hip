@@ -152,6 +152,160 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(const T* __restrict__ qkv
 }
 
 // ------------------------------------------------------------------------------------------------
+// Encoder self-attention, swapped-product form. One workgroup = 256 queries of one (window, head):
+// 8 waves x 32 queries; K/V tiles of 64 keys double-buffered in LDS (one barrier per tile, the next
+// tile's global loads in flight under the current tile's MFMAs).
+//   S^T[key][q] = K . Q^T     v_mfma_f32_32x32x16: A = K rows (ds_read_b128, XOR-swizzled image),
+//                             B = this wave's Q (registers, loaded once)
+//   softmax over keys         a lane holds 32 of the 64 keys of its query (lane^32 the other 32):
+//                             31 in-lane fmax + 1 exchange; row sums stay per lane until the end
+//   O^T[dim][q] += V^T . P^T  B = the S^T accumulator itself (registers 8s..8s+7 -> k-step s, in
+//                             the permuted key order of that layout), A = V^T via
+//                             ds_read_b64_tr_b16 from a row-major V image (no transposing store)
+// Exponentials in base 2 with the 1/8 scale and log2(e) folded into one FMA.
+template <typename T>
+__global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
+    typedef typename Frag<T>::type FT;
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int hh = lane >> 5, ql = lane & 31;
+    const long base = (long)b * Tn;
+    const int ld = 3 * d;
+    __shared__ u32x4 Ks[2][64 * 8];
+    __shared__ u32x4 Vs[2][64 * 8];
+    const u32x4 zero = {0, 0, 0, 0};
+
+    const int q = qb * 256 + wave * 32 + ql;
+    FT qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const u32x4 v = q < Tn ? *(const u32x4*)(qkv + (base + q) * ld + h * 64 + s * 16 + hh * 8) : zero;
+        qf[s] = __builtin_bit_cast(FT, v);
+    }
+    // staging: thread -> (key, 16-byte chunk) of the K and V tiles
+    const int skey = tid >> 3, sch = tid & 7;
+    const int k_slot = skey * 8 + (sch ^ ((skey >> 1) & 7));
+    const int v_slot = skey * 8 + (sch ^ (((skey >> 1) & 1) << 2));
+    auto load_kv = [&](int kt, u32x4& kv, u32x4& vv) {
+        const int kg = kt * 64 + skey;
+        kv = zero;
+        vv = zero;
+        if (kg < Tn) {
+            const T* src = qkv + (base + kg) * ld + h * 64 + sch * 8;
+            kv = *(const u32x4*)(src + d);
+            vv = *(const u32x4*)(src + 2 * d);
+        }
+    };
+    // transposed-read address (bytes within a V image) for rows r0..r0+3, this lane's dims
+    const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+    auto v_addr = [&](int r0, int db) {
+        const int row = r0 + tq;
+        const int ch = db * 4 + tg * 2 + (tp >> 1);
+        return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)) + 8 * (tp & 1);
+    };
+
+    f32x16 oacc[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) oacc[i][r] = 0.0f;
+    float m_run = -INFINITY, l_run = 0.0f;
+    const float c = 0.125f * 1.44269504088896340736f;
+
+    const int n_kt = (Tn + 63) / 64;
+    {
+        u32x4 kv, vv;
+        load_kv(0, kv, vv);
+        Ks[0][k_slot] = kv;
+        Vs[0][v_slot] = vv;
+    }
+    __syncthreads();
+    for (int kt = 0; kt < n_kt; kt++) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < n_kt;
+        u32x4 nk = zero, nv = zero;
+        if (more) load_kv(kt + 1, nk, nv);
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) sacc[kb][r] = 0.0f;
+            const int key = kb * 32 + ql;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const FT kf = __builtin_bit_cast(FT, Ks[cur][key * 8 + ((s * 2 + hh) ^ ((key >> 1) & 7))]);
+                sacc[kb] = mfma32x32x16(kf, qf[s], sacc[kb]);
+            }
+        }
+        if (kt * 64 + 64 > Tn) {
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int key = kt * 64 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    if (key >= Tn) sacc[kb][r] = -INFINITY;
+                }
+        }
+        float mx = sacc[0][0];
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) mx = fmaxf(mx, sacc[kb][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run, mx * c);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        FT pf[4];
+        float ls = 0.0f;
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+            for (int sp = 0; sp < 2; sp++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][sp * 8 + j], c, -m_new));
+                    ls += p;
+                    pf[kb * 2 + sp][j] = (T)p;
+                }
+        l_run = l_run * alpha + ls;
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) oacc[i][r] *= alpha;
+        const char* vimg = (const char*)Vs[cur];
+#pragma unroll
+        for (int db = 0; db < 2; db++)
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int r0 = (s >> 1) * 32 + (s & 1) * 16 + 4 * hh;
+                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + v_addr(r0, db)));
+                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + v_addr(r0 + 8, db)));
+                const FT vf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                oacc[db] = mfma32x32x16(vf, pf[s], oacc[db]);
+            }
+        if (more) {
+            Ks[cur ^ 1][k_slot] = nk;
+            Vs[cur ^ 1][v_slot] = nv;
+        }
+        __syncthreads();
+    }
+    if (q >= Tn) return;
+    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32));
+    T* orow = out + (base + q) * d + h * 64;
+#pragma unroll
+    for (int db = 0; db < 2; db++)
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) {
+            T v4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v4[j] = (T)(oacc[db][rr * 4 + j] * inv);
+            *(uint2*)(orow + db * 32 + rr * 8 + 4 * hh) = *(const uint2*)v4;
+        }
+}
+
+// ------------------------------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
                                                        const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
@@ -255,6 +409,16 @@ __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, 
 }
 
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st) {
+    static const int variant = [] {
+        const char* e = getenv("WHISPER_MI355X_ATTN");
+        return e ? atoi(e) : 2;
+    }();
+    if (variant == 2 && d == H * 64) {
+        dim3 grid(cdiv(Tn, 256), H, B);
+        if (dt == DType::F16) attn_enc2_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
+        else attn_enc2_kernel<bf16_t><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
+        return;
+    }
     dim3 grid(cdiv(Tn, 64), H, B);
     if (dt == DType::F16) attn_enc_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
     else attn_enc_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);

@@ -451,6 +451,100 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
     }
 }
 
+// Decode-step GEMM (M <= 128 active clips): one workgroup = all M rows x 64 columns x one K chunk
+// of up to 4 K-tiles. Every K-tile of the chunk is put in flight at once by LDS-DMA (up to 96 KiB
+// of LDS), so a workgroup pays one memory latency instead of one per K-tile; the grid is
+// (N/64) x splits with the partial tile written to the split-K slab (or through the epilogue
+// when the chunk is the whole K). Rows past M are clamped (their outputs are never stored).
+template <typename T, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const int kc) {
+    typedef typename Frag<T>::type FT;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int BM = 128, BN = 64, BK = 64, MAXT = 4;
+    constexpr int STAGE = (BM + BN) * 8;  // u32x4 per stage
+    __shared__ u32x4 lds[MAXT * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each 64 rows x 32 columns
+    const int n0 = blockIdx.x * BN;
+    const int k0 = SPLIT ? blockIdx.z * kc : 0;
+    const int nkt = min(kc, g.K - k0) / BK;
+    const T* A = (const T*)g.A;
+    const T* B = (const T*)g.B;
+    // per stage: A = 16 pieces of 8 rows (4 per wave), B = 8 pieces (2 per wave)
+    const T* a_src[4];
+    const T* b_src[2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int m = min(r, g.M - 1);
+        a_src[i] = A + (long)m * g.a_rstride + k0 + c * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int r = (wave * 2 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        const int n = min(n0 + r, g.N - 1);
+        b_src[i] = B + (long)n * g.K + k0 + c * 8;
+    }
+    for (int t = 0; t < nkt; t++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&lds[t * STAGE + (wave * 4 + i) * 64], 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK),
+                                             (lds_ptr_t)&lds[t * STAGE + BM * 8 + (wave * 2 + i) * 64], 16, 0, 0);
+    }
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nkt; t++) {
+        // this wave's DMAs of stages <= t have landed when at most 6*(nkt-1-t) are outstanding
+        const int left = nkt - 1 - t;
+        if (left >= 3) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
+        else if (left == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+        else if (left == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        const u32x4* st = &lds[t * STAGE];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            FT af[4], bfr[2];
+            const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = wm * 64 + i * 16 + (lane & 15);
+                af[i] = __builtin_bit_cast(FT, st[row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int row = wn * 32 + j * 16 + (lane & 15);
+                bfr[j] = __builtin_bit_cast(FT, st[BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+            if (n >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= g.M) continue;
+                if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+                else epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+            }
+        }
+}
+
 int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2
 
 template <typename T, int EPI>
@@ -458,6 +552,7 @@ __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
     const long total = (long)g.M * g.N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         float v = 0.0f;
+#pragma unroll 4
         for (int z = 0; z < splits; z++) v += g.splitk_ws[z * total + i];
         epilogue<EPI, T>(g, (int)(i / g.N), (int)(i % g.N), v);
     }
@@ -471,16 +566,27 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
     const int m = blockIdx.x, tid = threadIdx.x;
     const long total = (long)g.M * g.N;
     float* xrow = (float*)g.out + (long)m * g.ldo;
-    float v[NPT];
+    float a[NPT], v[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; k++) a[k] = 0.0f;
+    // z outer so each iteration has NPT independent loads in flight (same per-element z order)
+#pragma unroll 2
+    for (int z = 0; z < splits; z++) {
+        const float* w = g.splitk_ws + z * total + (long)m * g.N;
+#pragma unroll
+        for (int k = 0; k < NPT; k++) {
+            const int n = tid + 256 * k;
+            if (n < g.N) a[k] += w[n];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < NPT; k++) {
         const int n = tid + 256 * k;
         v[k] = 0.0f;
         if (n < g.N) {
-            float a = 0.0f;
-            for (int z = 0; z < splits; z++) a += g.splitk_ws[z * total + (long)m * g.N + n];
-            if (g.bias) a = a + g.bias[n];
-            const float x = a + xrow[n];
+            float x = a[k];
+            if (g.bias) x = x + g.bias[n];
+            x = x + xrow[n];
             xrow[n] = x;
             v[k] = x;
         }
@@ -508,6 +614,32 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
     }
     const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
     const int nk = cdiv(g.K, 64);
+    if (g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
+        // decode step, all K-tiles of a chunk in flight at once (gemm_dec_kernel): chunk <= 4
+        // K-tiles, split further (chunk >= 2 K-tiles) until the grid has >= 160 workgroups
+        const int tiles = cdiv(g.N, 64);
+        int splits = cdiv(nk, 4);
+        while (tiles * splits < 160 && (splits + 1) * 2 <= nk) splits++;
+        if ((long)splits * g.M * g.N <= g.splitk_ws_elems) {
+            const int kc = cdiv(nk, splits) * 64;
+            splits = cdiv(g.K, kc);
+            if (splits == 1 && !fused_ln) {
+                gemm_dec_kernel<T, EPI, false><<<tiles, 256, 0, st>>>(g, kc);
+                return;
+            }
+            gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            if (fused_ln) {
+                const int npt = cdiv(g.N, 256);
+                if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
+                else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
+                else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+            } else {
+                const long total = (long)g.M * g.N;
+                splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
+            }
+            return;
+        }
+    }
     if (g.splitk_ws && g.M <= 128) {
         // decode step (M = active clips <= 128): one M tile, the weight stream read exactly once;
         // K split to ~128 workgroups with >= 4 K-tiles each (partial slabs: M*N*splits*8 bytes)
