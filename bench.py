@@ -90,6 +90,22 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
                         f"{threads} OpenMP threads"))
 
 
+def rank_chunk_ids(rank: int, batch: int) -> list[int]:
+    """Weak-scaling shard: rank r transcribes chunks r*batch ... r*batch+batch-1 (independent
+    30 s chunks; no data-path exchange between ranks)."""
+    return [rank * batch + i for i in range(batch)]
+
+
+def max_over_ranks(x: float, dist, device: str) -> float:
+    """The timed region's wall time is the slowest rank's (contract: max over ranks)."""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,8 +167,8 @@ def main():
     buf = L.whisper_mi355x_dev_alloc(ctx.ptr, args.batch * n * 4)
     assert buf
     host = np.empty(n, np.float32)
-    for i in range(args.batch):
-        host[:] = synthetic_pcm(rank * args.batch + i)
+    for i, cid in enumerate(rank_chunk_ids(rank, args.batch)):
+        host[:] = synthetic_pcm(cid)
         L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(buf + i * n * 4), host.ctypes.data, n * 4, 1)
     jobs = [(buf + i * n * 4, n) for i in range(args.batch)]
     params = wrs.reference_full_params("en")
@@ -185,10 +201,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.time() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, dist, "cuda")
     out = (C.c_double * 3)()
     L.whisper_mi355x_kernel_stats(st.ptr, dom, out)
     k_ms, k_cnt, k_work = out[0], out[1], out[2]

@@ -451,11 +451,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
     }
 }
 
-// Decode-step GEMM (M <= 128 active clips): one workgroup = all M rows x 64 columns x one K chunk
-// of up to 4 K-tiles. Every K-tile of the chunk is put in flight at once by LDS-DMA (up to 96 KiB
-// of LDS), so a workgroup pays one memory latency instead of one per K-tile; the grid is
-// (N/64) x splits with the partial tile written to the split-K slab (or through the epilogue
-// when the chunk is the whole K). Rows past M are clamped (their outputs are never stored).
+// Decode-step GEMM (M <= 128 active clips): one workgroup = all M rows x 64 columns x one K chunk.
+// The chunk's K-tiles stream through a 4-deep LDS ring filled by LDS-DMA (96 KiB): four tiles are
+// in flight from the start and each consumed slot is refilled at once, so a workgroup pays about
+// one memory latency per four K-tiles. The grid is (N/64) x splits with the partial tile written
+// to the split-K slab (or through the epilogue when the chunk is the whole K). Rows past M are
+// clamped (their outputs are never stored).
 template <typename T, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const int kc) {
     typedef typename Frag<T>::type FT;
@@ -487,28 +488,29 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         const int n = min(n0 + r, g.N - 1);
         b_src[i] = B + (long)n * g.K + k0 + c * 8;
     }
-    for (int t = 0; t < nkt; t++) {
+    auto issue = [&](int t) {
+        u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
         for (int i = 0; i < 4; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&lds[t * STAGE + (wave * 4 + i) * 64], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&st[(wave * 4 + i) * 64], 16, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK),
-                                             (lds_ptr_t)&lds[t * STAGE + BM * 8 + (wave * 2 + i) * 64], 16, 0, 0);
-    }
+            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, 0);
+    };
+    for (int t = 0; t < min(nkt, MAXT); t++) issue(t);
     f32x4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < nkt; t++) {
-        // this wave's DMAs of stages <= t have landed when at most 6*(nkt-1-t) are outstanding
-        const int left = nkt - 1 - t;
-        if (left >= 3) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
-        else if (left == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
-        else if (left == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+        // this wave's DMAs of stage t have landed when at most 6 per later issued stage are outstanding
+        const int ahead = min(nkt - 1, t + MAXT - 1) - t;
+        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
+        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        const u32x4* st = &lds[t * STAGE];
+        const u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             FT af[4], bfr[2];
@@ -527,6 +529,10 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
             for (int i = 0; i < 4; i++)
 #pragma unroll
                 for (int j = 0; j < 2; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+        }
+        if (t + MAXT < nkt) {
+            __syncthreads();  // every wave is done with this slot
+            issue(t + MAXT);
         }
     }
 #pragma unroll
@@ -550,6 +556,23 @@ int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
     const long total = (long)g.M * g.N;
+    if ((g.N & 3) == 0) {  // 16-byte slab reads, 4 columns per thread (same per-element z order)
+        const long total4 = total >> 2;
+        for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+            for (int z = 0; z < splits; z++) {
+                const float4 w = ((const float4*)(g.splitk_ws + z * total))[i];
+                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+            }
+            const int m = (int)((i * 4) / g.N), n = (int)((i * 4) % g.N);
+            epilogue<EPI, T>(g, m, n, v.x);
+            epilogue<EPI, T>(g, m, n + 1, v.y);
+            epilogue<EPI, T>(g, m, n + 2, v.z);
+            epilogue<EPI, T>(g, m, n + 3, v.w);
+        }
+        return;
+    }
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         float v = 0.0f;
 #pragma unroll 4
@@ -570,7 +593,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
 #pragma unroll
     for (int k = 0; k < NPT; k++) a[k] = 0.0f;
     // z outer so each iteration has NPT independent loads in flight (same per-element z order)
-#pragma unroll 2
+#pragma unroll 4
     for (int z = 0; z < splits; z++) {
         const float* w = g.splitk_ws + z * total + (long)m * g.N;
 #pragma unroll
@@ -615,11 +638,11 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
     const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
     const int nk = cdiv(g.K, 64);
     if (g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
-        // decode step, all K-tiles of a chunk in flight at once (gemm_dec_kernel): chunk <= 4
-        // K-tiles, split further (chunk >= 2 K-tiles) until the grid has >= 160 workgroups
+        // decode step (gemm_dec_kernel): split K until the grid has >= 160 workgroups, chunks of
+        // >= 2 K-tiles and <= 8 splits (the reduce reads splits x M x N f32)
         const int tiles = cdiv(g.N, 64);
-        int splits = cdiv(nk, 4);
-        while (tiles * splits < 160 && (splits + 1) * 2 <= nk) splits++;
+        int splits = 1;
+        while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
         if ((long)splits * g.M * g.N <= g.splitk_ws_elems) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
