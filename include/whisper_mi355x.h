@@ -75,6 +75,12 @@ WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cl
 WHISPER_API int whisper_mi355x_debug_gemm(struct whisper_context * ctx, int epi, const void * A, int M, int K,
                                           const void * B, int N, const float * bias, void * out, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_gemm_variant(int variant);
+WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
+/* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
+ * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */
+WHISPER_API int whisper_mi355x_debug_gemm_ln(struct whisper_context * ctx, const void * A, int M, int K,
+                                             const void * B, int N, const float * bias, float * x,
+                                             const float * ln_w, const float * ln_b, void * y, int reps, float * ms);
 
 /* ABI self-description, no device needed: sizeof(whisper_full_params), sizeof(whisper_context_params),
  * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /

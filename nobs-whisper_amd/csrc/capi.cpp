@@ -10,7 +10,7 @@
 #include "../../include/whisper_mi355x.h"
 #include "engine.h"
 
-namespace wm { extern int g_gemm_variant; }
+namespace wm { extern int g_gemm_variant; extern int g_dec_splits; }
 using namespace wm;
 
 static Context* C(whisper_context* ctx) { return ctx ? &ctx->c : nullptr; }
@@ -472,6 +472,7 @@ int whisper_mi355x_kernel_stats(struct whisper_state* s, int cls, double out[3])
 // ---- kernel-level test/tuning hooks ---------------------------------------------------------------
 
 void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
+void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
 // out[M][N] (f32 for epi EPI_F32 / EPI_RESID, else the context dtype) = A[M][K] . B[N][K]^T + bias,
 // all device pointers; runs `reps` times and returns the average ms per launch in *ms.
 int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B, int N,
@@ -504,6 +505,37 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
     hipEventDestroy(e1);
     hipStreamDestroy(st);
     if (g.splitk_ws) hipFree(g.splitk_ws);
+    return 0;
+}
+int whisper_mi355x_debug_gemm_ln(struct whisper_context* ctx, const void* A, int M, int K, const void* B, int N,
+                                 const float* bias, float* x, const float* ln_w, const float* ln_b, void* y, int reps,
+                                 float* ms) {
+    if (!ctx || M > 128) return -1;
+    hipSetDevice(ctx->c.device);
+    hipStream_t st;
+    WM_CHECK(hipStreamCreate(&st));
+    GemmArgs g{};
+    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+    g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.out = x; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
+    g.splitk_ws_elems = 64L * M * N;
+    WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+    hipEvent_t e0, e1;
+    WM_CHECK(hipEventCreate(&e0));
+    WM_CHECK(hipEventCreate(&e1));
+    WM_CHECK(hipEventRecord(e0, st));
+    for (int r = 0; r < std::max(1, reps); r++) launch_gemm(ctx->c.dt, EPI_RESID, g, st);
+    WM_CHECK(hipEventRecord(e1, st));
+    WM_CHECK(hipStreamSynchronize(st));
+    float t = 0;
+    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+    if (ms) *ms = t / std::max(1, reps);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipStreamDestroy(st);
+    hipFree(g.splitk_ws);
     return 0;
 }
 // ABI self-description (no device needed): sizes/offsets that a binding generator must agree on.

@@ -27,18 +27,34 @@ static hipEvent_t kt_event(whisper_state* s) {
     WM_CHECK(hipEventCreate(&e));
     return e;
 }
+// Record a timing event on the state's stream. While a decode step is being captured, the record
+// is added as an explicit event-record node of the graph: a stream-captured hipEventRecord does
+// not yield a timestamp on replay (hipEventElapsedTime -> invalid handle), an explicit node does
+// (tools/probe/graph_events.hip).
+static void kt_record(whisper_state* s, hipEvent_t e) {
+    if (!s->capture_ev) { WM_CHECK(hipEventRecord(e, s->stream)); return; }
+    hipStreamCaptureStatus cs;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    WM_CHECK(hipStreamGetCaptureInfo_v2(s->stream, &cs, &id, &g, &deps, &nd));
+    hipGraphNode_t node;
+    WM_CHECK(hipGraphAddEventRecordNode(&node, g, deps, nd, e));
+    WM_CHECK(hipStreamUpdateCaptureDependencies(s->stream, &node, 1, hipStreamSetCaptureDependencies));
+}
 struct KT {
     whisper_state* s;
     int cls;
     double work;
     hipEvent_t a = nullptr;
     KT(whisper_state* s_, int c, double w) : s(s_), cls(c), work(w) {
-        if ((s->ktime_mask >> c) & 1) { a = kt_event(s); WM_CHECK(hipEventRecord(a, s->stream)); }
+        if ((s->ktime_mask >> c) & 1) { a = kt_event(s); kt_record(s, a); }
     }
     ~KT() {
         if (!a) return;
         hipEvent_t b = kt_event(s);
-        WM_CHECK(hipEventRecord(b, s->stream));
+        kt_record(s, b);
         (s->capture_ev ? *s->capture_ev : s->kpending).push_back({cls, a, b, work});
     }
 };
@@ -54,7 +70,13 @@ static void kt_flush_graph(whisper_state* s, const whisper_state::DecGraph& g) {
     for (auto& p : g.ev) {
         if (!((s->ktime_mask >> p.cls) & 1)) continue;
         float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) continue;
+        const hipError_t e = hipEventElapsedTime(&ms, p.a, p.b);
+        if (e != hipSuccess) {
+            static bool warned = false;
+            if (!warned) fprintf(stderr, "whisper_mi355x: graph kernel timing unavailable (%s)\n", hipGetErrorString(e));
+            warned = true;
+            continue;
+        }
         s->kstat[p.cls].ms += ms;
         s->kstat[p.cls].work += p.cls == K_ATTN_SELF ? s->cur_self_work : p.work;
         s->kstat[p.cls].count++;
@@ -373,7 +395,7 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
         }
         {
             KT kt(s, K_ATTN_SELF, s->cur_self_work);
-            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
+            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, false, st);
         }
         resid(w.datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
         {
@@ -383,7 +405,7 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
         }
         {
             KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);
-            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
+            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, true, st);
         }
         resid(w.datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
         tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, w.dff, 4 * d), st);

@@ -59,7 +59,7 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int
 // single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:
 // token i attends keys [0, n_kv[i]) of slot[i]; q [n][q_stride] at head h offset h*64; out [n][d]
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
-                        int n, int L, int layer, int H, int ctx, int d, void* out, hipStream_t st);
+                        int n, int L, int layer, int H, int ctx, int d, void* out, bool cross, hipStream_t st);
 
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {

@@ -306,7 +306,8 @@ __global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qk
 }
 
 // ------------------------------------------------------------------------------------------------
-template <typename T>
+// CROSS only separates the symbols of the two uses (self / cross cache) in profiles.
+template <typename T, bool CROSS>
 __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
                                                        const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
                                                        int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
@@ -425,16 +426,20 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
 }
 
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv, int n,
-                        int L, int layer, int H, int ctx, int d, void* out, hipStream_t st) {
+                        int L, int layer, int H, int ctx, int d, void* out, bool cross, hipStream_t st) {
     if (n <= 0) return;
     if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
     dim3 grid(n, H);
-    if (dt == DType::F16)
-        attn_dec_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, q_stride, (const half_t*)cache, slot, n_kv, L, layer,
-                                                      H, ctx, d, (half_t*)out);
-    else
-        attn_dec_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)cache, slot, n_kv, L,
-                                                      layer, H, ctx, d, (bf16_t*)out);
+#define WM_ATTN_DEC(TT, CR) \
+    attn_dec_kernel<TT, CR><<<grid, 256, 0, st>>>((const TT*)q, q_stride, (const TT*)cache, slot, n_kv, L, layer, H, ctx, d, (TT*)out)
+    if (dt == DType::F16) {
+        if (cross) WM_ATTN_DEC(half_t, true);
+        else WM_ATTN_DEC(half_t, false);
+    } else {
+        if (cross) WM_ATTN_DEC(bf16_t, true);
+        else WM_ATTN_DEC(bf16_t, false);
+    }
+#undef WM_ATTN_DEC
 }
 
 }  // namespace wm

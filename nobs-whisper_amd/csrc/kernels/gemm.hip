@@ -617,6 +617,80 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
     block256_layernorm<T, NPT>(v, g.N, g.ln_w, g.ln_b, (T*)g.ln_out + (long)m * g.N, sh);
 }
 
+// Same contract as splitk_reduce_resid_ln_kernel for N % 4 == 0, N <= 4096: one thread per 4
+// consecutive columns (16-byte slab reads, all splits in flight at once), ceil(N/256) waves per row.
+template <typename T>
+__global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const GemmArgs g, int splits) {
+    __shared__ double sh[16];
+    const int m = blockIdx.x, tid = threadIdx.x, nw = blockDim.x >> 6;
+    const long total = (long)g.M * g.N;
+    const int n = tid * 4;
+    const bool on = n < g.N;
+    float x[4] = {0.f, 0.f, 0.f, 0.f};
+    if (on) {
+        const float* w = g.splitk_ws + (long)m * g.N + n;
+#pragma unroll 8
+        for (int z = 0; z < splits; z++) {
+            const float4 p = *(const float4*)(w + z * total);
+            x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
+        }
+        float4* xr = (float4*)((float*)g.out + (long)m * g.ldo + n);
+        const float4 r = *xr;
+        if (g.bias) {
+            const float4 b = *(const float4*)(g.bias + n);
+            x[0] = x[0] + b.x; x[1] = x[1] + b.y; x[2] = x[2] + b.z; x[3] = x[3] + b.w;
+        }
+        x[0] = x[0] + r.x; x[1] = x[1] + r.y; x[2] = x[2] + r.z; x[3] = x[3] + r.w;
+        *xr = make_float4(x[0], x[1], x[2], x[3]);
+    }
+    // ggml_norm: double sums, float mean / variance, (v*scale)*w + b separately rounded
+    auto block_sum = [&](double v) {
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((tid & 63) == 0) sh[tid >> 6] = v;
+        __syncthreads();
+        double r = 0.0;
+        for (int i = 0; i < nw; i++) r += sh[i];
+        __syncthreads();
+        return r;
+    };
+    double s = on ? (((double)x[0] + (double)x[1]) + (double)x[2]) + (double)x[3] : 0.0;
+    s = block_sum(s);
+    const float mean = (float)(s / g.N);
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        x[k] = __fsub_rn(x[k], mean);
+        s2 += (double)__fmul_rn(x[k], x[k]);
+    }
+    s2 = block_sum(on ? s2 : 0.0);
+    const float variance = (float)(s2 / g.N);
+    const float scale = 1.0f / sqrtf(variance + 1e-5f);
+    if (!on) return;
+    const float4 w4 = *(const float4*)(g.ln_w + n);
+    const float4 b4 = *(const float4*)(g.ln_b + n);
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
+    T y[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) y[k] = (T)__fadd_rn(__fmul_rn(__fmul_rn(x[k], scale), wv[k]), bv[k]);
+    *(uint2*)((T*)g.ln_out + (long)m * g.N + n) = *(const uint2*)y;
+}
+
+int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
+static int dec_splits_override() { return g_dec_splits; }
+
+template <typename T>
+static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st) {
+    if (g.N % 4 == 0 && g.N <= 4096) {
+        const int threads = cdiv(g.N / 4, 64) * 64;
+        splitk_reduce_resid_ln4_kernel<T><<<g.M, threads, 0, st>>>(g, splits);
+        return;
+    }
+    const int npt = cdiv(g.N, 256);
+    if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
+    else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
+    else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+}
+
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     const bool big256 = g_gemm_variant == 2 || (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
@@ -643,7 +717,11 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int tiles = cdiv(g.N, 64);
         int splits = 1;
         while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
-        if ((long)splits * g.M * g.N <= g.splitk_ws_elems) {
+        if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
+        // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
+        // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
+        const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64;
+        if ((long)splits * g.M * g.N <= g.splitk_ws_elems && !small_unsplit) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
@@ -652,10 +730,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             }
             gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
             if (fused_ln) {
-                const int npt = cdiv(g.N, 256);
-                if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
-                else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
-                else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+                launch_reduce_resid_ln<T>(g, splits, st);
             } else {
                 const long total = (long)g.M * g.N;
                 splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);

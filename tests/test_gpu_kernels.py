@@ -60,3 +60,39 @@ def test_gemm_matches_numpy(wrs, ctx, M, N, K, variant):
     bound = 1e-4 * (np.abs(A64) @ np.abs(B64).T) + 1e-5
     err = np.abs(out - ref)
     assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (37, 384, 1536), (128, 1280, 5120), (128, 1280, 1280), (64, 1024, 4096)])
+def test_gemm_resid_ln_matches_numpy(wrs, ctx, M, N, K):
+    """Decode-step residual GEMM + fused LayerNorm (split-K slabs -> reduce + residual + LN)."""
+    L = wrs.lib()
+    L.whisper_mi355x_debug_gemm_ln.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                               C.POINTER(C.c_float)]
+    rng = np.random.default_rng(M * 3 + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float16)
+    B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    x = rng.standard_normal((M, N)).astype(np.float32)
+    w = (1.0 + 0.1 * rng.standard_normal(N)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(N)).astype(np.float32)
+    y = np.zeros((M, N), np.float16)
+    ptrs = [_dev(wrs, ctx, a) for a in (A, B, bias, x, w, b, y)]
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_gemm_ln(ctx.ptr, C.c_void_p(ptrs[0]), M, K, C.c_void_p(ptrs[1]), N, C.c_void_p(ptrs[2]),
+                                          C.c_void_p(ptrs[3]), C.c_void_p(ptrs[4]), C.c_void_p(ptrs[5]),
+                                          C.c_void_p(ptrs[6]), 1, C.byref(ms)) == 0
+    xo = np.empty_like(x)
+    L.whisper_mi355x_memcpy(ctx.ptr, xo.ctypes.data, C.c_void_p(ptrs[3]), xo.nbytes, 2)
+    L.whisper_mi355x_memcpy(ctx.ptr, y.ctypes.data, C.c_void_p(ptrs[6]), y.nbytes, 2)
+    for p in ptrs:
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    A64, B64 = A.astype(np.float64), B.astype(np.float64)
+    xr = x + A64 @ B64.T + bias
+    bound = 1e-4 * (np.abs(A64) @ np.abs(B64).T) + 1e-5 + 1e-6 * np.abs(xr)
+    assert (np.abs(xo - xr) <= bound).all(), f"residual max err {np.abs(xo - xr).max()}"
+    mu = xr.mean(1, keepdims=True)
+    var = ((xr - mu) ** 2).mean(1, keepdims=True)
+    yr = (xr - mu) / np.sqrt(var + 1e-5) * w + b
+    err = np.abs(y.astype(np.float64) - yr)
+    assert (err <= 2e-3 + 2e-3 * np.abs(yr)).all(), f"LN max err {err.max()}"
