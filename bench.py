@@ -90,6 +90,31 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
                         f"{threads} OpenMP threads"))
 
 
+# kernel symbols of each class in the rocprofv3 PMC output (tools/pmc.sh -> tools/pmc_traffic.py)
+K_SYMBOL = {"gemm_encoder": r"gemm256_kernel", "attn_encoder": r"attn_enc2_kernel",
+            "attn_cross_decode": r"attn_cross_step_kernel"}
+
+
+def pmc_traffic(kernel_class: str):
+    """Launch-weighted HBM bytes per launch of the class's kernel from the newest committed
+    profiles/*_pmc_traffic.json (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE), or
+    None when no PMC pass covers it."""
+    import glob
+    import re
+    pat = K_SYMBOL.get(kernel_class)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not pat or not files:
+        return None, None
+    with open(files[-1]) as f:
+        data = json.load(f)
+    n = tb = 0.0
+    for sym, v in data.items():
+        if re.search(pat, sym):
+            n += v["launches"]
+            tb += v["traffic_bytes"] * v["launches"]
+    return (tb / n if n else None), os.path.basename(files[-1])
+
+
 def rank_chunk_ids(rank: int, batch: int) -> list[int]:
     """Weak-scaling shard: rank r transcribes chunks r*batch ... r*batch+batch-1 (independent
     30 s chunks; no data-path exchange between ranks)."""
@@ -219,6 +244,10 @@ def main():
             achieved = k_work / (k_ms * 1e-3) / 1e9
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
+        traffic, src = pmc_traffic(K_NAMES[dom])
+        if traffic is not None:
+            roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                        traffic_source=f"profiles/{src}")
         roof.update(kernel=K_NAMES[dom], launches=int(k_cnt), avg_launch_ms=round(k_ms / max(1, k_cnt), 4),
                     work_per_launch=k_work / max(1, k_cnt), time_share_warmup=share)
         cpu = None

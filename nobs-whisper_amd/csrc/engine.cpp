@@ -384,28 +384,43 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
         launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
         launch_layernorm(dt, w.dx, nullptr, n_tok, d, W.dec[0].ln1_w, W.dec[0].ln1_b, w.dh, st);
     }
+    // decode steps: the QKV and cross-Q projections leave split-K partial sums that the attention
+    // kernels reduce in their prologue (no separate reduce launch)
+    auto partials = [&](const void* A, const void* Wt, int N, const float* bias, float scale) -> DecSlabs {
+        GemmArgs g = gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N);
+        g.splitk_ws = w.splitk;
+        g.splitk_ws_elems = w.splitk_elems;
+        KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N);
+        const int splits = launch_gemm_partials(dt, g, st);
+        if (splits <= 0) { fprintf(stderr, "whisper_mi355x: decode partials GEMM not applicable\n"); abort(); }
+        return DecSlabs{w.splitk, splits, (long)n_tok * N, N, bias, scale};
+    };
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
-        {
+        if (fused) {
+            const DecSlabs sl = partials(w.dh, Lw.wqkv, 3 * d, Lw.bqkv, c->k_scale);
+            KT kt(s, K_ATTN_SELF, s->cur_self_work);
+            launch_attn_self_step(dt, sl, w.self, w.slot, w.pos, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
+        } else {
             GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wqkv, 3 * d, Lw.bqkv, w.dq, d);
             g.scale = c->k_scale;
             g.cache = w.self; g.row_slot = w.slot; g.row_pos = w.pos; g.L = L; g.layer = l; g.H = H;
             g.ctx = hp.n_text_ctx; g.d = d;
             tgemm(s, KCLS, dt, EPI_QKV_DEC, g, st);
-        }
-        {
             KT kt(s, K_ATTN_SELF, s->cur_self_work);
-            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, false, st);
+            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, 0, st);
         }
         resid(w.datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
-        {
+        if (fused) {
+            const DecSlabs sl = partials(w.dh, Lw.wxq, d, Lw.bxq, c->k_scale);
+            KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);  // the class holds decode steps only
+            launch_attn_cross_step(dt, sl, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
+        } else {
             GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
             tgemm(s, KCLS, dt, EPI_STORE, g, st);
-        }
-        {
-            KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);
-            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, true, st);
+            KT kt(s, K_OTHER, (double)n_tok * hp.n_audio_ctx * kvrow);
+            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, 2, st);
         }
         resid(w.datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
         tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, w.dff, 4 * d), st);

@@ -52,6 +52,10 @@ struct GemmArgs {
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
+// Decode step (M <= 128, K % 64 == 0): only the split-K partial sums, slabs [splits][M][N] f32 in
+// a.splitk_ws, no epilogue; the consumer reduces them (attention prologues). Returns the split
+// count, or 0 when the shape/workspace does not allow it (the caller then uses launch_gemm).
+int launch_gemm_partials(DType dt, const GemmArgs& a, hipStream_t st);
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------
 // encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)
@@ -59,7 +63,21 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int
 // single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:
 // token i attends keys [0, n_kv[i]) of slot[i]; q [n][q_stride] at head h offset h*64; out [n][d]
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
-                        int n, int L, int layer, int H, int ctx, int d, void* out, bool cross, hipStream_t st);
+                        int n, int L, int layer, int H, int ctx, int d, void* out, int kind, hipStream_t st);
+
+// Decode-step attention with the projection GEMM's split-K reduce fused into its prologue.
+// Slab z holds rows [M][ld] of partial sums; the value of (row i, column c) is
+// sum_z ws[z*zstride + i*ld + c] + bias[c] (the same order as the standalone reduce).
+struct DecSlabs {
+    const float* ws; int splits; long zstride; int ld; const float* bias; float scale;
+};
+// self attention of token i: q/k/v columns [0,d)/[d,2d)/[2d,3d) of the QKV slabs (q and k scaled,
+// as the EPI_QKV_DEC epilogue); writes this position's k, v into the self cache at pos[i].
+void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int* slot, const int* pos, int n, int L,
+                           int layer, int H, int ctx, int d, void* out, hipStream_t st);
+// cross attention of token i over n_kv[i] keys of the cross cache; q from the cross-Q slabs.
+void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
+                            int L, int layer, int H, int ctx, int d, void* out, hipStream_t st);
 
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {

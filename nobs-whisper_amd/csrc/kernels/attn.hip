@@ -306,11 +306,13 @@ __global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qk
 }
 
 // ------------------------------------------------------------------------------------------------
-// CROSS only separates the symbols of the two uses (self / cross cache) in profiles.
-template <typename T, bool CROSS>
-__global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
-                                                       const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
-                                                       int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
+// FQ: q is not read from a buffer but reduced from the cross-Q projection's split-K slabs
+// (DecSlabs; q = (T)((sum_z + bias) * scale), the EPI_STORE epilogue of that GEMM).
+template <typename T, bool FQ>
+__device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_stride, const DecSlabs sl,
+                                              const T* __restrict__ cache, const int* __restrict__ slot,
+                                              const int* __restrict__ n_kv_arr, int L, int layer, int H, int ctx, int d,
+                                              T* __restrict__ out) {
     const int i = blockIdx.x, h = blockIdx.y;
     const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3;  // 32 groups of 8 lanes
     const int n_kv = n_kv_arr[i];
@@ -322,7 +324,19 @@ __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, 
     __shared__ float acc_s[32][65];
 
     float qv[8];
-    {
+    if constexpr (FQ) {
+        if (tid < 64) {
+            const float* p = sl.ws + (long)i * sl.ld + h * 64 + tid;
+            float v = 0.0f;
+            for (int z = 0; z < sl.splits; z++) v += p[z * sl.zstride];
+            if (sl.bias) v = v + sl.bias[h * 64 + tid];
+            red[tid] = (float)(T)(v * sl.scale);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 8; e++) qv[e] = red[lane8 * 8 + e];
+        __syncthreads();
+    } else {
         const u32x4 raw = *(const u32x4*)(q + (long)i * q_stride + h * 64 + lane8 * 8);
         const T* qe = (const T*)&raw;
 #pragma unroll
@@ -409,6 +423,160 @@ __global__ void __launch_bounds__(256) attn_dec_kernel(const T* __restrict__ q, 
     }
 }
 
+// One body, three kernel names so profiles separate the uses: the self cache (prefill), the cross
+// cache in a decode step (one token per clip, q reduced from slabs: the roofline kernel) and the
+// cross cache in a prefill.
+template <typename T>
+__global__ void __launch_bounds__(256) attn_self_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
+                                                        const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
+                                                        int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
+    attn_dec_body<T, false>(q, q_stride, DecSlabs{}, cache, slot, n_kv_arr, L, layer, H, ctx, d, out);
+}
+template <typename T>
+__global__ void __launch_bounds__(256) attn_cross_prefill_kernel(const T* __restrict__ q, int q_stride,
+                                                                 const T* __restrict__ cache, const int* __restrict__ slot,
+                                                                 const int* __restrict__ n_kv_arr, int L, int layer, int H,
+                                                                 int ctx, int d, T* __restrict__ out) {
+    attn_dec_body<T, false>(q, q_stride, DecSlabs{}, cache, slot, n_kv_arr, L, layer, H, ctx, d, out);
+}
+template <typename T>
+__global__ void __launch_bounds__(256) attn_cross_step_kernel(const DecSlabs sl, const T* __restrict__ cache,
+                                                              const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
+                                                              int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
+    attn_dec_body<T, true>(nullptr, 0, sl, cache, slot, n_kv_arr, L, layer, H, ctx, d, out);
+}
+
+// Decode-step self attention, one wave per (token, head), HPB heads per workgroup. The prologue
+// reduces this token's q, k, v from the QKV projection's split-K slabs (EPI_QKV_DEC arithmetic: q
+// and k scaled, rounded to T), appends k, v to the self cache at pos[i] and attends keys
+// [0, pos) from the cache plus the fresh key from registers. Scores: 8 lanes per key row (16 B
+// each), U rows in flight per lane group; softmax and P.V reductions are wave shuffles.
+template <typename T, int HPB>
+__global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs sl, T* __restrict__ cache,
+                                                                  const int* __restrict__ slot,
+                                                                  const int* __restrict__ pos_arr, int L, int layer,
+                                                                  int H, int ctx, int d, T* __restrict__ out) {
+    const int i = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int h = blockIdx.y * HPB + w;
+    const int lane8 = lane & 7, grp = lane >> 3;  // 8 groups of 8 lanes
+    __shared__ float qs[HPB][64], ks[HPB][64], vs[HPB][64];
+    __shared__ float sc[HPB][448];
+    const int pos = pos_arr[i];
+    const long s = slot[i];
+    T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
+    T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
+    {
+        const float* p = sl.ws + (long)i * sl.ld + h * 64 + lane;
+        float vq = 0.0f, vk = 0.0f, vv = 0.0f;
+        for (int z = 0; z < sl.splits; z++) {
+            const float* pz = p + z * sl.zstride;
+            vq += pz[0];
+            vk += pz[d];
+            vv += pz[2 * d];
+        }
+        if (sl.bias) {
+            vq = vq + sl.bias[h * 64 + lane];
+            vk = vk + sl.bias[d + h * 64 + lane];
+            vv = vv + sl.bias[2 * d + h * 64 + lane];
+        }
+        const T tq = (T)(vq * sl.scale), tk = (T)(vk * sl.scale), tv = (T)vv;
+        K[(long)pos * 64 + lane] = tk;
+        V[(long)pos * 64 + lane] = tv;
+        qs[w][lane] = (float)tq;
+        ks[w][lane] = (float)tk;
+        vs[w][lane] = (float)tv;
+    }
+    __syncthreads();
+    float qv[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
+    constexpr int U = 4;
+    const u32x4 zero = {0, 0, 0, 0};
+    float lmax = -INFINITY;
+    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            raw[u] = t < pos ? *(const u32x4*)(K + (long)t * 64 + lane8 * 8) : zero;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const T* ke = (const T*)&raw[u];
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+            a += __shfl_xor(a, 1);
+            a += __shfl_xor(a, 2);
+            a += __shfl_xor(a, 4);
+            if (t < pos) {
+                if (lane8 == 0) sc[w][t] = a;
+                lmax = fmaxf(lmax, a);
+            }
+        }
+    }
+    {  // the fresh key (position pos)
+        float a = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) a += qv[e] * ks[w][lane8 * 8 + e];
+        a += __shfl_xor(a, 1);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 4);
+        if (lane == 0) sc[w][pos] = a;
+        lmax = fmaxf(lmax, a);
+    }
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    __syncthreads();
+    const int n_kv = pos + 1;
+    float lsum = 0.0f;
+    for (int t = lane; t < n_kv; t += 64) {
+        const float e = expf(sc[w][t] - lmax);
+        sc[w][t] = e;
+        lsum += e;
+    }
+    for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o);
+    const float inv = 1.0f / lsum;
+    for (int t = lane; t < n_kv; t += 64) sc[w][t] = (float)(T)(sc[w][t] * inv);  // P rounded as ggml's f16 src1
+    __syncthreads();
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] = 0.0f;
+    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            raw[u] = t < pos ? *(const u32x4*)(V + (long)t * 64 + lane8 * 8) : zero;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const T* ve = (const T*)&raw[u];
+            const float p = t < pos ? sc[w][t] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+        }
+    }
+    if (grp == 0) {
+        const float p = sc[w][pos];
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc[e] += p * vs[w][lane8 * 8 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        acc[e] += __shfl_xor(acc[e], 8);
+        acc[e] += __shfl_xor(acc[e], 16);
+        acc[e] += __shfl_xor(acc[e], 32);
+    }
+    if (grp == 0) {
+        T o8[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) o8[e] = (T)acc[e];
+        *(u32x4*)(out + (long)i * d + h * 64 + lane8 * 8) = *(const u32x4*)o8;
+    }
+}
+
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st) {
     static const int variant = [] {
         const char* e = getenv("WHISPER_MI355X_ATTN");
@@ -426,20 +594,46 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
 }
 
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv, int n,
-                        int L, int layer, int H, int ctx, int d, void* out, bool cross, hipStream_t st) {
+                        int L, int layer, int H, int ctx, int d, void* out, int kind, hipStream_t st) {
     if (n <= 0) return;
     if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
     dim3 grid(n, H);
-#define WM_ATTN_DEC(TT, CR) \
-    attn_dec_kernel<TT, CR><<<grid, 256, 0, st>>>((const TT*)q, q_stride, (const TT*)cache, slot, n_kv, L, layer, H, ctx, d, (TT*)out)
+#define WM_ATTN_DEC(TT, KN) \
+    KN<TT><<<grid, 256, 0, st>>>((const TT*)q, q_stride, (const TT*)cache, slot, n_kv, L, layer, H, ctx, d, (TT*)out)
     if (dt == DType::F16) {
-        if (cross) WM_ATTN_DEC(half_t, true);
-        else WM_ATTN_DEC(half_t, false);
+        if (kind == 2) WM_ATTN_DEC(half_t, attn_cross_prefill_kernel);
+        else WM_ATTN_DEC(half_t, attn_self_kernel);
     } else {
-        if (cross) WM_ATTN_DEC(bf16_t, true);
-        else WM_ATTN_DEC(bf16_t, false);
+        if (kind == 2) WM_ATTN_DEC(bf16_t, attn_cross_prefill_kernel);
+        else WM_ATTN_DEC(bf16_t, attn_self_kernel);
     }
 #undef WM_ATTN_DEC
+}
+
+void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
+                            int L, int layer, int H, int ctx, int d, void* out, hipStream_t st) {
+    if (n <= 0) return;
+    if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
+    dim3 grid(n, H);
+    if (dt == DType::F16)
+        attn_cross_step_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)cache, slot, n_kv, L, layer, H, ctx, d, (half_t*)out);
+    else
+        attn_cross_step_kernel<bf16_t><<<grid, 256, 0, st>>>(sl, (const bf16_t*)cache, slot, n_kv, L, layer, H, ctx, d, (bf16_t*)out);
+}
+
+void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int* slot, const int* pos, int n, int L,
+                           int layer, int H, int ctx, int d, void* out, hipStream_t st) {
+    if (n <= 0) return;
+    if (ctx > 448) { fprintf(stderr, "whisper_mi355x: self-attention context %d > 448\n", ctx); abort(); }
+    const int hpb = H % 4 == 0 ? 4 : H % 2 == 0 ? 2 : 1;
+#define WM_SELF(TT, HB) \
+    attn_self_step_kernel<TT, HB><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
+#define WM_SELF_H(TT) \
+    do { if (hpb == 4) WM_SELF(TT, 4); else if (hpb == 2) WM_SELF(TT, 2); else WM_SELF(TT, 1); } while (0)
+    if (dt == DType::F16) WM_SELF_H(half_t);
+    else WM_SELF_H(bf16_t);
+#undef WM_SELF_H
+#undef WM_SELF
 }
 
 }  // namespace wm

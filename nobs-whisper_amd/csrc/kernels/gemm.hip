@@ -352,7 +352,10 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const GemmArgs g, const 
 // 256x256x64 tiles, 8 waves (2 x 4), each wave 128x64 (8 x 4 MFMA 16x16x32 tiles, 128 accumulator
 // registers): twice the MFMA work per barrier of the 128x128 kernel and 0.375 LDS fragment reads
 // per MFMA. Same LDS-DMA staging, swizzle and XCD remap; 2 stages x 64 KiB LDS, one block per CU.
-template <typename T, int EPI>
+// PIPE: fragment reads of the next k-step are issued under the current k-step's MFMAs (two
+// register sets), one barrier per K-tile placed between the two k-steps; the DMA of tile t+2 is
+// issued right after that barrier into the buffer tile t has just released.
+template <typename T, int EPI, bool PIPE>
 __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const int tiles_n) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -393,6 +396,45 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nk = g.K / BK;
+    if constexpr (PIPE) {
+        auto read_frags = [&](int buf, int s, FT (&af)[8], FT (&bfr)[4]) {
+            const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int row = wn * 64 + j * 16 + (lane & 15);
+                bfr[j] = __builtin_bit_cast(FT, lds[buf][BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int row = wm * 128 + i * 16 + (lane & 15);
+                af[i] = __builtin_bit_cast(FT, lds[buf][row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+        };
+        auto mfmas = [&](const FT (&af)[8], const FT (&bfr)[4]) {
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+            __builtin_amdgcn_s_setprio(0);
+        };
+        FT a0[8], b0[4], a1[8], b1[4];
+        issue(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (nk > 1) issue(1, 1);
+        read_frags(0, 0, a0, b0);
+        for (int kt = 0; kt < nk; kt++) {
+            const int cur = kt & 1;
+            read_frags(cur, 1, a1, b1);  // k-step 1 of this tile, under k-step 0's MFMAs
+            mfmas(a0, b0);
+            // tile kt+1 landed (this wave's DMA), every wave done reading tile kt
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (kt + 2 < nk) issue(cur, kt + 2);
+            if (kt + 1 < nk) read_frags(cur ^ 1, 0, a0, b0);  // next tile's k-step 0, under k-step 1
+            mfmas(a1, b1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
     issue(0, 0);
     for (int kt = 0; kt < nk; kt++) {
         const int cur = kt & 1;
@@ -424,6 +466,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
             __builtin_amdgcn_s_setprio(0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     }
     // epilogue: each wave transposes its 128x64 tile through LDS 16 rows at a time so every lane
     // owns 16 consecutive columns of one row (16-byte stores instead of 4-byte column stores)
@@ -551,7 +594,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         }
 }
 
-int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2
+int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2, 3 same, pipelined
 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
@@ -693,10 +736,12 @@ static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
-    const bool big256 = g_gemm_variant == 2 || (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
+    const bool big256 = g_gemm_variant == 2 || g_gemm_variant == 3 ||
+                        (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && big256) {
         const int tn = cdiv(g.N, 256);
-        gemm256_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        else gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
@@ -797,6 +842,24 @@ static void launch_dt(int epi, const GemmArgs& g, hipStream_t st) {
         case EPI_QKV_DEC: launch_t<T, EPI_QKV_DEC>(g, st); break;
         default: fprintf(stderr, "whisper_mi355x: bad epilogue %d\n", epi); abort();
     }
+}
+
+template <typename T>
+static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
+    if (!g.splitk_ws || g.M > 128 || g.K % 64 != 0) return 0;
+    const int nk = g.K / 64, tiles = cdiv(g.N, 64);
+    int splits = 1;
+    while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+    if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
+    const int kc = cdiv(nk, splits) * 64;
+    splits = cdiv(g.K, kc);
+    if ((long)splits * g.M * g.N > g.splitk_ws_elems) return 0;
+    gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    return splits;
+}
+
+int launch_gemm_partials(DType dt, const GemmArgs& g, hipStream_t st) {
+    return dt == DType::F16 ? launch_partials_t<half_t>(g, st) : launch_partials_t<bf16_t>(g, st);
 }
 
 void launch_gemm(DType dt, int epi, const GemmArgs& g, hipStream_t st) {

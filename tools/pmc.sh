@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM traffic of the roofline kernels from PMC counters (GPU box). Two separate passes, FETCH_SIZE
+# and WRITE_SIZE (they do not fit one TCC pass), counters only (no sys/runtime trace), each on a
+# short bench run (same per-launch work as the full bench: cross-attention always reads 1500 keys).
+# Output: gpurun_out/pmc_{fetch,write}/ CSVs; tools/pmc_traffic.py turns them into bytes/launch.
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd /tmp && export TMPDIR=/tmp
+ARGS="--tokens 4 --steps 1 --warmup 1 --cpu-baseline 0"
+REGEX="${PMC_REGEX:-attn_cross_step_kernel|gemm256_kernel|attn_enc2_kernel}"
+for c in FETCH_SIZE WRITE_SIZE; do
+  d="$R/gpurun_out/pmc_$(echo $c | tr A-Z a-z | cut -d_ -f1)"
+  timeout -k 10 ${T_PMC:-500} rocprofv3 --pmc $c --kernel-include-regex "$REGEX" --output-format csv -d "$d" -o run \
+      -- python3 "$R/bench.py" $ARGS > "$d.log" 2>&1
+  rc=$?; echo "pmc $c rc=$rc"; tail -3 "$d.log"
+  [ $rc -eq 0 ] || exit $rc
+done
