@@ -82,6 +82,17 @@ WHISPER_API int whisper_mi355x_debug_gemm_ln(struct whisper_context * ctx, const
                                              const void * B, int N, const float * bias, float * x,
                                              const float * ln_w, const float * ln_b, void * y, int reps, float * ms);
 
+/* Debug/tuning: the direct cross attention of decode steps (Q' projection, one pass over the
+ * encoder output per token, split merge + value projection) on caller data, device pointers in the
+ * context's compute type: enc [slots][n_ctx][d], slot [n] (int), q [n][d] (already scaled by
+ * d_head^-0.25), wkt [d/64][d][64] (cross K weights per head, transposed), wv [d][d], bv [d] (f32)
+ * -> out [n][d]. splits <= 0 picks the engine's split count; rescale_thr is the online-softmax
+ * lazy-rescale threshold in log2 units (the engine uses 8). */
+WHISPER_API int whisper_mi355x_debug_xattn(struct whisper_context * ctx, const void * enc, const int * slot,
+                                           const void * q, const void * wkt, const void * wv, const float * bv,
+                                           int n, int n_ctx, int d, float scale, int splits, float rescale_thr,
+                                           void * out, int reps, float * ms);
+
 /* ABI self-description, no device needed: sizeof(whisper_full_params), sizeof(whisper_context_params),
  * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /
  * new_segment_callback / vad_params). Lets a binding (bindgen, ctypes) be checked field-by-field. */

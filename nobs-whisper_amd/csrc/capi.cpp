@@ -538,6 +538,48 @@ int whisper_mi355x_debug_gemm_ln(struct whisper_context* ctx, const void* A, int
     hipFree(g.splitk_ws);
     return 0;
 }
+// Direct cross attention (kernels/xattn.hip: Q' projection, one pass over E, split merge + Wv) on
+// caller data, all device pointers in the context dtype: enc [slots][n_ctx][d], slot [n] int,
+// q [n][d] (already scaled), wkt [H][d][64], wv [d][d], bv [d] f32 -> out [n][d].
+int whisper_mi355x_debug_xattn(struct whisper_context* ctx, const void* enc, const int* slot, const void* q,
+                               const void* wkt, const void* wv, const float* bv, int n, int n_ctx, int d, float scale,
+                               int splits, float rescale_thr, void* out, int reps, float* ms) {
+    if (!ctx || n <= 0 || !xattn_supported(d)) return -1;
+    hipSetDevice(ctx->c.device);
+    const DType dt = ctx->c.dt;
+    const int H = d / 64;
+    if (splits <= 0) splits = xattn_splits(n, n_ctx);
+    void* qx = nullptr;
+    float *op = nullptr, *ml = nullptr;
+    WM_CHECK(hipMalloc(&qx, (size_t)n * 2 * H * d * 2));
+    WM_CHECK(hipMalloc((void**)&op, (size_t)n * splits * H * d * 4));
+    WM_CHECK(hipMalloc((void**)&ml, (size_t)n * splits * H * 2 * 4));
+    hipStream_t st;
+    WM_CHECK(hipStreamCreate(&st));
+    auto run = [&] {
+        launch_xattn_qproj(dt, q, wkt, n, d, H, scale, qx, st);
+        launch_xattn_step(dt, enc, slot, qx, n, n_ctx, d, splits, rescale_thr, op, ml, st);
+        launch_xattn_combine(dt, op, ml, splits, wv, bv, n, d, H, out, st);
+    };
+    hipEvent_t e0, e1;
+    WM_CHECK(hipEventCreate(&e0));
+    WM_CHECK(hipEventCreate(&e1));
+    run();
+    WM_CHECK(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++) run();
+    WM_CHECK(hipEventRecord(e1, st));
+    WM_CHECK(hipStreamSynchronize(st));
+    float t = 0;
+    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+    if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipStreamDestroy(st);
+    hipFree(qx);
+    hipFree(op);
+    hipFree(ml);
+    return 0;
+}
 // ABI self-description (no device needed): sizes/offsets that a binding generator must agree on.
 int whisper_mi355x_abi_layout(size_t out[8]) {
     out[0] = sizeof(whisper_full_params);

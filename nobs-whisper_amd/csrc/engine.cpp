@@ -119,7 +119,8 @@ static void free_ws(Workspace& w) {
     // sub-allocations (pos/slot/.. of tok, win_seek/win_slot of win_job, pcm_ptrs/n_* of mel_ptrs)
     // are freed with their parent
     void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
-                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk};
+                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk,
+                  w.enc, w.qx, w.xo, w.xml, w.kvslot};
     for (void* p : ps) dfree(p);
     if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
     if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
@@ -136,6 +137,12 @@ void free_state(whisper_state* s) {
     hipStreamDestroy(s->stream);
     delete s;
 }
+
+// prefills with at most this many tokens per clip take the direct cross attention; longer prompts
+// go through a cross K/V cache computed for their clips on demand
+static const int kXDirectMaxTok = 8;
+// lazy-rescale threshold of the direct cross attention's online softmax (log2 units: P <= 2^8)
+static const float kXattnThr = 8.0f;
 
 static int enc_batch_cap() {
     const char* e = getenv("WHISPER_MI355X_ENC_BATCH");
@@ -171,14 +178,35 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         const int L = hp.n_text_layer;
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         for (void* p : {w.cross, w.self, (void*)w.dx, w.dh, w.dq, w.datt, w.dff, w.lrow, (void*)w.logits, (void*)w.probs,
-                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs, (void*)w.splitk})
+                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs, (void*)w.splitk, w.enc, w.qx,
+                        (void*)w.xo, (void*)w.xml, (void*)w.kvslot})
             dfree(p);
+        w.cross = w.enc = w.qx = nullptr;
+        w.xo = w.xml = nullptr;
         w.splitk_elems = 16L * std::min(n_tok, 256) * 4 * (long)d;
         WM_CHECK(hipMalloc((void**)&w.splitk, w.splitk_elems * 4));
         if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
         if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
         if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
-        WM_CHECK(hipMalloc(&w.cross, (size_t)n_jobs * L * 2 * T * d * E));
+        if (c->cross_direct) {
+            // no cross K/V cache up front: decode steps (and short prefills) read E directly
+            const int H = hp.n_text_head;
+            w.cap_xq = std::max(kXDirectMaxTok * n_jobs, 128);
+            const size_t xo_rows = std::max(w.cap_xq, 512);  // n * xattn_splits(n) <= max(n, 511)
+            WM_CHECK(hipMalloc(&w.enc, (size_t)n_jobs * T * d * E));
+            WM_CHECK(hipMalloc(&w.qx, (size_t)w.cap_xq * 2 * H * d * E));
+            WM_CHECK(hipMalloc((void**)&w.xo, xo_rows * H * d * 4));
+            WM_CHECK(hipMalloc((void**)&w.xml, xo_rows * H * 2 * 4));
+        } else {
+            WM_CHECK(hipMalloc(&w.cross, (size_t)n_jobs * L * 2 * T * d * E));
+        }
+        w.cross_fresh.assign(n_jobs, 0);
+        {
+            std::vector<int> ident(n_jobs);
+            for (int k = 0; k < n_jobs; k++) ident[k] = k;
+            WM_CHECK(hipMalloc((void**)&w.kvslot, (size_t)n_jobs * sizeof(int)));
+            WM_CHECK(hipMemcpy(w.kvslot, ident.data(), (size_t)n_jobs * sizeof(int), hipMemcpyHostToDevice));
+        }
         WM_CHECK(hipMalloc(&w.self, (size_t)n_jobs * L * 2 * hp.n_text_ctx * d * E));
         WM_CHECK(hipMalloc((void**)&w.dx, (size_t)n_tok * d * 4));
         WM_CHECK(hipMalloc(&w.dh, (size_t)n_tok * d * E));
@@ -286,6 +314,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
     Workspace& w = s->ws;
     const int d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, H = hp.n_audio_head;
     const DType dt = c->dt;
+    const size_t E = esize(dt);
     const int KCLS = K_GEMM_ENC;
     const Weights& W = c->w;
     hipStream_t st = s->stream;
@@ -327,8 +356,15 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
             tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, L.w2, d, L.b2, w.x, d), st);
         }
         launch_layernorm(dt, w.x, nullptr, M, d, W.lnpost_w, W.lnpost_b, w.hn, st);
-        // cross K/V of every decoder layer in one GEMM, scattered into each window's slot
-        {
+        if (c->cross_direct) {
+            // keep E per slot for the direct cross attention; the slot's cross K/V (if any) is stale
+            for (int k = 0; k < nb; k++) {
+                WM_CHECK(hipMemcpyAsync((char*)w.enc + (size_t)slots[b0 + k] * T * d * E, (const char*)w.hn + (size_t)k * T * d * E,
+                                        (size_t)T * d * E, hipMemcpyDeviceToDevice, st));
+                w.cross_fresh[slots[b0 + k]] = 0;
+            }
+        } else {
+            // cross K/V of every decoder layer in one GEMM, scattered into each window's slot
             GemmArgs g = gemm_plain(w.hn, M, d, W.wkv_cross, 2 * hp.n_text_layer * d, W.bkv_cross, nullptr, 0);
             g.scale = c->k_scale;
             g.cache = w.cross; g.row_slot = d_slot; g.L = hp.n_text_layer; g.H = hp.n_text_head; g.ctx = T; g.d = d;
@@ -363,7 +399,7 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) 
 // the decoder forward over n_tok tokens + logits of n_rows rows; kernels only (graph-capturable).
 // Decode steps (one token per clip, logits for every row, <= 128 rows) take the fused path: every
 // LayerNorm is folded into the embedding or into the split-K reduce of the preceding residual GEMM.
-static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity) {
+static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
     const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
@@ -411,7 +447,28 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
             launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, 0, st);
         }
         resid(w.datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
-        if (fused) {
+        if (xdirect) {
+            // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
+            // -> one pass over E per clip -> split merge + Wv
+            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
+            g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
+            tgemm(s, KCLS, dt, EPI_STORE, g, st);
+            const int Ta = hp.n_audio_ctx, S = xattn_splits(n_tok, Ta);
+            {
+                KT kt(s, KCLS, 2.0 * d * d + 2.0 * n_tok * d + 4.0 * n_tok * H * d);
+                launch_xattn_qproj(dt, w.dq, (const char*)W.wkT + (size_t)l * H * d * 64 * 2, n_tok, d, H, c->k_scale, w.qx, st);
+            }
+            {
+                // the roofline class holds decode steps only (E bytes read once per clip and layer)
+                KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2);
+                launch_xattn_step(dt, w.enc, w.slot, w.qx, n_tok, Ta, d, S, kXattnThr, w.xo, w.xml, st);
+            }
+            {
+                KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d);
+                launch_xattn_combine(dt, w.xo, w.xml, S, (const char*)W.wkv_cross + (size_t)(2 * l + 1) * d * d * 2,
+                                     W.bkv_cross + (size_t)(2 * l + 1) * d, n_tok, d, H, w.datt, st);
+            }
+        } else if (fused) {
             const DecSlabs sl = partials(w.dh, Lw.wxq, d, Lw.bxq, c->k_scale);
             KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);  // the class holds decode steps only
             launch_attn_cross_step(dt, sl, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
@@ -436,9 +493,45 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
     }
 }
 
+// Cross K/V of the given slots (all decoder layers, one GEMM per clip) into the cache, for slots
+// whose cache is stale: direct mode computes it only for prompts too long for the direct prefill.
+static void ensure_cross_cache(Context* c, whisper_state* s, const std::vector<int>& slots) {
+    Workspace& w = s->ws;
+    const Hparams& hp = c->hp;
+    const int d = hp.n_audio_state, T = hp.n_audio_ctx, L = hp.n_text_layer;
+    const size_t E = esize(c->dt);
+    if (!w.cross) WM_CHECK(hipMalloc(&w.cross, (size_t)w.cap_jobs * L * 2 * T * d * E));
+    for (int sl : slots) {
+        if (w.cross_fresh[sl]) continue;
+        GemmArgs g = gemm_plain((const char*)w.enc + (size_t)sl * T * d * E, T, d, c->w.wkv_cross, 2 * L * d, c->w.bkv_cross,
+                                nullptr, 0);
+        g.scale = c->k_scale;
+        g.cache = w.cross; g.row_slot = w.kvslot + sl; g.L = L; g.H = hp.n_text_head; g.ctx = T; g.d = d;
+        tgemm(s, K_GEMM_ENC, c->dt, EPI_CROSSKV, g, s->stream);
+        w.cross_fresh[sl] = 1;
+    }
+}
+
+// Direct cross attention for this forward (tokens/slots already in w.h_ints)? Yes for one-token
+// steps and short prompts; otherwise the clips involved get a cross K/V cache first.
+static bool choose_xdirect(Context* c, whisper_state* s, int n_tok) {
+    if (!c->cross_direct) return false;
+    Workspace& w = s->ws;
+    const int* slot = w.h_ints + 2 * w.cap_tok;
+    std::vector<int> cnt(w.cap_jobs, 0);
+    int mx = 0;
+    for (int i = 0; i < n_tok; i++) mx = std::max(mx, ++cnt[slot[i]]);
+    if (n_tok <= w.cap_xq && mx <= kXDirectMaxTok) return true;
+    std::vector<int> used;
+    for (int k = 0; k < w.cap_jobs; k++) if (cnt[k]) used.push_back(k);
+    ensure_cross_cache(c, s, used);
+    return false;
+}
+
 static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity = false) {
+    const bool xdirect = choose_xdirect(c, s, n_tok);
     decoder_upload(c, s, n_tok, n_rows);
-    decoder_launch(c, s, n_tok, n_rows, rows_identity);
+    decoder_launch(c, s, n_tok, n_rows, rows_identity, xdirect);
 }
 
 int decode_tokens(Context* c, whisper_state* s, const int* tokens, const int* pos, const int* slots, int n_tok,
@@ -725,7 +818,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     decoder_upload(c, s, n, n);
     const bool any = logits_prepare(S, act, false);
     if (!use_graphs()) {
-        decoder_launch(c, s, n, n, true);
+        decoder_launch(c, s, n, n, true, c->cross_direct);
         logits_launch(c, s, n);
         logits_finish(S, n, any, probs_rows);
         return;
@@ -738,7 +831,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        decoder_launch(c, s, n, n, true);
+        decoder_launch(c, s, n, n, true, c->cross_direct);
         logits_launch(c, s, n);
         WM_CHECK(hipStreamEndCapture(s->stream, &graph));
         s->capture_ev = nullptr;

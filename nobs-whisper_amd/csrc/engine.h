@@ -55,6 +55,7 @@ struct Weights {
     void* tok_emb; float* pos_d;
     float *lnd_w, *lnd_b;
     void* wkv_cross; float* bkv_cross;  // [L_d][2][d][d], bias [L_d][2][d] (K part zero)
+    void* wkT = nullptr;                // [L_d][H][d][64]: cross K per head, transposed (direct cross attention)
     std::vector<LayerW> enc, dec;
     void* mel_tab;    // MelTablesDev (sin, cos, hann)
     float* filt_t;    // [201][n_mels]
@@ -75,6 +76,9 @@ struct Context {
     whisper_timings timings{};
     whisper_state* default_state = nullptr;  // whisper_init_from_file_with_params (with state)
     float k_scale = 0.0f;                    // d_head^-0.25
+    // Cross attention straight from the encoder output (kernels/xattn.hip) instead of through a
+    // materialised cross K/V cache; set at load (WHISPER_MI355X_CROSS=cache turns it off).
+    bool cross_direct = false;
     std::string model_type;
     whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
 };
@@ -98,8 +102,16 @@ struct Workspace {
     // encoder (cap_enc windows)
     void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
     float* x = nullptr;
-    // caches (cap_jobs slots)
+    // caches (cap_jobs slots). In direct mode `cross` is allocated on first use (prompts too long
+    // for the direct prefill) and cross_fresh[slot] says whether a slot's cross K/V match enc.
     void *cross = nullptr, *self = nullptr;
+    std::vector<char> cross_fresh;
+    int* kvslot = nullptr;  // identity [cap_jobs]: row_slot of a one-clip cross-KV GEMM
+    // direct cross attention: encoder output per slot [cap_jobs][T][d], Q' [cap_xq][2H][d],
+    // split partials [xo_rows][H][d] f32 + [xo_rows][H][2]
+    void *enc = nullptr, *qx = nullptr;
+    float *xo = nullptr, *xml = nullptr;
+    int cap_xq = 0;
     // decoder (cap_tok tokens)
     float* dx = nullptr;
     void *dh = nullptr, *dq = nullptr, *datt = nullptr, *dff = nullptr, *lrow = nullptr;

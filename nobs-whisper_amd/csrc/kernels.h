@@ -79,6 +79,22 @@ void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int*
 void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
                             int L, int layer, int H, int ctx, int d, void* out, hipStream_t st);
 
+// ---- cross attention from the encoder output (kernels/xattn.hip) --------------------------------
+// enc [slot][Tn][d] (the encoder's ln_post output in the MFMA type). For token i (clip slot[i]):
+//   qproj:   qx[i][h][:] / qx[i][H+h][:] = hi / lo parts of scale * Wk_h^T q[i][h*64:(h+1)*64]
+//            (wkt = Wk per head, transposed: [H][d][64]);
+//   step:    rows split sp: unnormalised partial O^T opart[i][sp][h][d] and ml[i][sp][h] = {m (log2 units), l};
+//            the running max moves only when a tile exceeds it by more than thr (log2 units);
+//   combine: out[i][h*64+j] = (sum_sp w_sp O_sp / L) . Wv[h*64+j][:] + bv[h*64+j]   (MFMA type)
+bool xattn_supported(int d);
+int xattn_splits(int n, int Tn);
+void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
+                        hipStream_t st);
+void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
+                       float thr, float* opart, float* ml, hipStream_t st);
+void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
+                          int d, int H, void* out, hipStream_t st);
+
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {
     int n_vocab, eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, space, n_lang;

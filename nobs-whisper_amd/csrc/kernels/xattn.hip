@@ -1,0 +1,454 @@
+// Decode-step cross attention computed straight from the encoder output (SURVEY.md §8a row a10,
+// the roofline kernel of the headline benchmark).
+//
+// whisper.cpp caches K = s*(E.Wk^T) and V = E.Wv^T + bv for every decoder layer ([ext] kv_cross)
+// and each decode step reads both: 2 x 1500 x d values per clip and layer. Both products are linear
+// in the encoder output E [1500][d], so per head h the same scores and outputs are
+//   score_t  = q_h . K_h[t]            = E[t] . Q'_h,   Q'_h = s * Wk_h^T q_h        (d values)
+//   o_h      = sum_t p_t V_h[t] / l    = (sum_t p_t E[t] / l) . Wv_h^T + bv_h
+// so a step needs ONE pass over E per clip and layer instead of a pass over K and one over V:
+// half the HBM bytes of the cached form, and no 31 GB cross cache at batch 128. The extra work is
+// MFMA work (E [16 rows][d] x Q' [d][2H] and P [H][16] x E [16][d] per tile), which this
+// HBM-bound step has to spare.
+//
+//   xattn_qproj_kernel    Q'_h = s * Wk_h^T q_h for every head, split into hi + lo parts of the
+//                         MFMA type so the scores keep ~16 mantissa bits (Q' rows 0..H-1 = hi,
+//                         H..2H-1 = lo); a batched [n x 64] . [64 x d] GEMM per head.
+//   xattn_step_kernel     one workgroup = one clip x one split of the 1500 rows; E tiles of 16
+//                         rows stream HBM -> LDS by LDS-DMA (3 stages, two tiles in flight across
+//                         raw barriers); each wave owns CT x 32 columns: partial scores
+//                         S^T[16][2H] (v_mfma_16x16x32, A = E rows), a cross-wave reduce in LDS,
+//                         online softmax per head (lazy rescale: the running max moves only when
+//                         a tile exceeds it by more than `thr` in log2 units), then
+//                         O^T[cols][heads] += E^T . P^T (v_mfma_32x32x16, A = E^T by
+//                         ds_read_b64_tr_b16 from the same LDS image). Writes the unnormalised
+//                         partial O, m and l of its split.
+//   xattn_combine_kernel  merges the splits, E~ = sum_s w_s O_s / L (hi + lo parts again), and
+//                         applies Wv_h + bv: o[i][h*64+j] in the MFMA type, the input of the
+//                         cross-attention output projection.
+//
+// Roofline: HBM-bound on E: 1500 x d x 2 bytes per clip and layer (3.84 MB for large-v3).
+// Numerics vs whisper.cpp: no rounding of K and V to the cache type (the products are formed in
+// f32 from the same rounded E and weights), P rounded to the MFMA type as ggml rounds it to f16
+// (here before the final 1/l instead of after it).
+#include <algorithm>
+
+#include "../common.h"
+#include "../kernels.h"
+
+namespace wm {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// 16-byte chunk swizzle inside each 256-byte group of an LDS row: conflict-free for ds_read_b128
+// of 16 rows x one chunk and for ds_read_b64_tr_b16 of 4 rows x 2 chunks (guide T10 image (b)).
+__device__ __forceinline__ int xsw(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int xphys(int row, int ch) { return (ch & ~15) | ((ch & 15) ^ xsw(row)); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ v4s ds_read_tr(unsigned lds_addr) {
+    v4s r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr));
+    return r;
+}
+// LDS writes of this wave done, then the workgroup barrier. A raw s_barrier, not __syncthreads():
+// the latter waits vmcnt(0) and would drain the LDS-DMA tiles kept in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---- Q' projection -----------------------------------------------------------------------------
+// grid (d/64, H, cdiv(n, 64)), 256 threads: wave w = tokens [z*64 + 16w, +16) x 64 columns.
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ q, const T* __restrict__ wkt, int n, int d,
+                                                          int H, float scale, T* __restrict__ qx) {
+    typedef typename Frag<T>::type FT;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c0 = blockIdx.x * 64, h = blockIdx.y;
+    const int i0 = blockIdx.z * 64 + wave * 16;
+    if (i0 >= n) return;  // wave-uniform
+    const u32x4 zero = {0, 0, 0, 0};
+    const int ia = i0 + (lane & 15);
+    FT af[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++)
+        af[ks] = __builtin_bit_cast(FT, ia < n ? *(const u32x4*)(q + (long)ia * d + h * 64 + ks * 32 + 8 * (lane >> 4)) : zero);
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int c = c0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+            const FT bf = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + c) * 64 + ks * 32 + 8 * (lane >> 4)));
+            acc[j] = mfma16x16x32(af[ks], bf, acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int c = c0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = i0 + 4 * (lane >> 4) + r;
+            if (i >= n) continue;
+            const float v = acc[j][r] * scale;
+            const T hi = (T)v;
+            const T lo = (T)(v - (float)hi);
+            qx[((long)i * 2 * H + h) * d + c] = hi;
+            qx[((long)i * 2 * H + H + h) * d + c] = lo;
+        }
+    }
+}
+
+// ---- one pass over E per (clip, split) ------------------------------------------------------------
+// NW waves x CT column tiles of 32: d = NW*CT*32, H = d/64, NQ = ceil(2H/16) score column tiles.
+template <typename T, int NW, int CT>
+__global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
+                                                             const T* __restrict__ qx, int Tn, int splits, float thr,
+                                                             float* __restrict__ opart, float* __restrict__ ml) {
+    typedef typename Frag<T>::type FT;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
+    constexpr int RC = D / 8;            // 16-byte chunks per E row
+    constexpr int NS = 3;                // LDS stages
+    constexpr int TILE = 16 * RC;        // u32x4 per 16-row tile
+    constexpr int RSR = 16 * NQ + 4;     // f32 row stride of the score partials (bank spread)
+    constexpr int STG_B = NS * TILE * 16, RED_B = NW * 16 * RSR * 4, P_B = 32 * 16 * (int)sizeof(T);
+    static_assert(RC % 16 == 0, "d must be a multiple of 128");
+    static_assert(H * 16 <= NW * 64, "one softmax lane per (head, row)");
+    static_assert(H <= 32, "heads are the N = 32 side of the P.V MFMA");
+    // ONE LDS object (a second __shared__ object can make hipcc wait vmcnt(0) before LDS reads)
+    __shared__ __attribute__((aligned(16))) char lds[STG_B + RED_B + P_B + 32 * 4 + 16];
+    u32x4* stg = (u32x4*)lds;
+    float* red = (float*)(lds + STG_B);
+    T* pimg = (T*)(lds + STG_B + RED_B);              // P [head][16 rows]
+    float* alph = (float*)(lds + STG_B + RED_B + P_B);  // per-head rescale of the tile
+    int* flag = (int*)(alph + 32);                      // [2]: some head rescaled at tile t (parity t&1)
+
+    const int sp = blockIdx.x, i = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nt_all = (Tn + 15) >> 4;
+    const int tb = sp * nt_all / splits, ntile = (sp + 1) * nt_all / splits - tb;
+    const T* E = enc + (long)slot[i] * Tn * D;
+    const int cw = wave * CT * 32;  // this wave's first column
+
+    for (int e = tid; e < 32 * 16; e += NW * 64) pimg[e] = (T)0.0f;
+    if (tid < 32) alph[tid] = 1.0f;
+    if (tid < 2) flag[tid] = 0;
+
+    // Q' fragments (B operand of the scores): head' = j*16 + (lane&15), 8 columns per lane
+    const u32x4 zero = {0, 0, 0, 0};
+    FT qf[CT][NQ];
+    {
+        const T* Q = qx + (long)i * 2 * H * D;
+#pragma unroll
+        for (int kk = 0; kk < CT; kk++)
+#pragma unroll
+            for (int j = 0; j < NQ; j++) {
+                const int hp = j * 16 + (lane & 15);
+                qf[kk][j] = __builtin_bit_cast(
+                    FT, hp < 2 * H ? *(const u32x4*)(Q + (long)hp * D + cw + kk * 32 + 8 * (lane >> 4)) : zero);
+            }
+        // consume the loads here, before any LDS-DMA is issued, so hipcc's wait for them sits outside the loop
+#pragma unroll
+        for (int kk = 0; kk < CT; kk++)
+#pragma unroll
+            for (int j = 0; j < NQ; j++) asm volatile("" ::"v"(qf[kk][j]));
+    }
+    // LDS-DMA sources: piece p = wave + k*NW (64 chunks), lane -> physical chunk -> (row, logical chunk)
+    int prow[CT], poff[CT];
+#pragma unroll
+    for (int k = 0; k < CT; k++) {
+        const int qq = (wave + k * NW) * 64 + lane;
+        const int row = qq / RC, pc = qq - row * RC;
+        prow[k] = row;
+        poff[k] = xphys(row, pc) * 8;
+    }
+    auto issue = [&](int t) {
+        const int row0 = (tb + t) * 16;
+        u32x4* st = stg + (t % NS) * TILE;
+#pragma unroll
+        for (int k = 0; k < CT; k++) {
+            const int gr = min(row0 + prow[k], Tn - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]), (lds_ptr_t)(st + (wave + k * NW) * 64),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 oacc[CT];
+#pragma unroll
+    for (int k = 0; k < CT; k++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) oacc[k][r] = 0.0f;
+    float m_run = -INFINITY, l_run = 0.0f;  // softmax lanes (tid < 16H): head tid>>4
+    const float LOG2E = 1.44269504088896340736f;
+    const int hh = lane >> 5;
+
+    issue(0);
+    if (ntile > 1) issue(1);
+    for (int t = 0; t < ntile; t++) {
+        // B1: tile t landed (this wave's pieces), every wave left tile t-1 (stage (t+2)%3 is free)
+        if (t + 1 < ntile) wait_vm<CT>();
+        else wait_vm<0>();
+        lds_barrier();
+        if (t + 2 < ntile) issue(t + 2);
+        const u32x4* st = stg + (t % NS) * TILE;
+
+        // scores: S^T[row][head'] over this wave's columns
+        f32x4 sacc[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; j++) sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        {
+            const int row = lane & 15;
+#pragma unroll
+            for (int kk = 0; kk < CT; kk++) {
+                const int ch = (cw >> 3) + kk * 4 + (lane >> 4);
+                const FT ef = __builtin_bit_cast(FT, st[row * RC + xphys(row, ch)]);
+#pragma unroll
+                for (int j = 0; j < NQ; j++) sacc[j] = mfma16x16x32(ef, qf[kk][j], sacc[j]);
+            }
+        }
+        {
+            float* rw = red + wave * 16 * RSR;
+#pragma unroll
+            for (int j = 0; j < NQ; j++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) rw[(4 * (lane >> 4) + r) * RSR + j * 16 + (lane & 15)] = sacc[j][r];
+        }
+        lds_barrier();  // B2: partial scores of every wave in LDS
+
+        // online softmax, one lane per (head, row); hi + lo partials summed in a fixed order
+        if (tid < 16 * H) {
+            const int h = tid >> 4, r = tid & 15;
+            float sv = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const float* rr = red + (w * 16 + r) * RSR;
+                sv += rr[h];
+                sv += rr[H + h];
+            }
+            const float s2 = (tb + t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
+            float mx = s2;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            float alpha = 1.0f;
+            if (mx > m_run + thr) {  // first tile (m_run = -inf) or the max moved by more than thr
+                alpha = __builtin_amdgcn_exp2f(m_run - mx);
+                m_run = mx;
+                flag[t & 1] = 1;
+            }
+            const T pt = (T)__builtin_amdgcn_exp2f(s2 - m_run);
+            float ps = (float)pt;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) ps += __shfl_xor(ps, o);
+            l_run = l_run * alpha + ps;
+            pimg[h * 16 + r] = pt;
+            if (r == 0) alph[h] = alpha;
+        }
+        if (tid == 0) flag[(t + 1) & 1] = 0;  // last read in tile t-1's P.V, before B1
+        lds_barrier();  // B3: P, alpha and the flag in LDS
+
+        // O^T[cols][heads] += E^T . P^T  (every lane active: the transposed reads need EXEC = all ones)
+        if (flag[t & 1]) {
+            const float al = alph[lane & 31];
+#pragma unroll
+            for (int k = 0; k < CT; k++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) oacc[k][r] *= al;
+        }
+        FT pf;
+        {
+            const T* pr = pimg + (lane & 31) * 16 + 4 * hh;
+            const v4s lo = *(const v4s*)pr;
+            const v4s hi = *(const v4s*)(pr + 8);
+            pf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        {
+            // E^T fragments by inline-asm ds_read_b64_tr_b16: with an LDS-DMA in flight hipcc puts
+            // vmcnt(0) in front of the builtin form (it cannot rule out the DMA writing the bytes it
+            // reads), which would drain the prefetch of tile t+2; the DMA/read ordering here is the
+            // explicit vmcnt + barrier of B1.
+            const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+            const int rlo = 4 * hh + tq, rhi = rlo + 8;
+            const unsigned img = (unsigned)(unsigned long)(lds_ptr_t)(const void*)st;
+            v4s lo[CT], hi[CT];
+#pragma unroll
+            for (int k = 0; k < CT; k++) {
+                const int ch = ((cw + k * 32) >> 3) + tg * 2 + (tp >> 1);
+                lo[k] = ds_read_tr(img + rlo * RC * 16 + 16 * xphys(rlo, ch) + 8 * (tp & 1));
+                hi[k] = ds_read_tr(img + rhi * RC * 16 + 16 * xphys(rhi, ch) + 8 * (tp & 1));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs behind the wait (guide §5.4 rule 18)
+#pragma unroll
+            for (int k = 0; k < CT; k++) {
+                const FT ef = __builtin_bit_cast(FT, __builtin_shufflevector(lo[k], hi[k], 0, 1, 2, 3, 4, 5, 6, 7));
+                oacc[k] = mfma32x32x16(ef, pf, oacc[k]);
+            }
+        }
+    }
+
+    // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2]
+    const int h = lane & 31;
+    if (h < H) {
+        float* o = opart + (((long)i * splits + sp) * H + h) * D;
+#pragma unroll
+        for (int k = 0; k < CT; k++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int c = cw + k * 32 + 8 * g + 4 * hh;
+                *(float4*)(o + c) = make_float4(oacc[k][4 * g], oacc[k][4 * g + 1], oacc[k][4 * g + 2], oacc[k][4 * g + 3]);
+            }
+    }
+    if (tid < 16 * H && (tid & 15) == 0) {
+        float* p = ml + (((long)i * splits + sp) * H + (tid >> 4)) * 2;
+        p[0] = m_run;
+        p[1] = l_run;
+    }
+}
+
+// ---- merge the splits and apply Wv ---------------------------------------------------------------
+// grid (H, cdiv(n, 16)), 256 threads: wave w sums columns [w*d/4, (w+1)*d/4) for 16 tokens x 64
+// outputs; M = 32 rows (E~ hi for the 16 tokens, then lo), N = 64, K = d/4; waves reduced in LDS.
+// m is in log2 units (the step kernel scales scores by log2 e).
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_combine_kernel(const float* __restrict__ opart, const float* __restrict__ ml,
+                                                            int splits, const T* __restrict__ wv, const float* __restrict__ bv,
+                                                            int n, int d, int H, T* __restrict__ out) {
+    typedef typename Frag<T>::type FT;
+    const int h = blockIdx.x, i0 = blockIdx.y * 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ float wgt[16][16];
+    __shared__ float acc_s[4][32][65];
+    if (tid < 16) {
+        const int i = i0 + tid;
+        if (i < n) {
+            const float* p = ml + ((long)i * splits * H + h) * 2;
+            float M = -INFINITY;
+            for (int s = 0; s < splits; s++) M = fmaxf(M, p[(long)s * H * 2]);
+            float L = 0.0f;
+            for (int s = 0; s < splits; s++) L += __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * p[(long)s * H * 2 + 1];
+            const float inv = 1.0f / L;
+            for (int s = 0; s < splits; s++) wgt[tid][s] = __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * inv;
+        } else {
+            for (int s = 0; s < splits; s++) wgt[tid][s] = 0.0f;
+        }
+    }
+    __syncthreads();
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int i = min(i0 + r16, n - 1);
+    const float* src = opart + ((long)i * splits * H + h) * d;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[a][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int kw = d / 4;
+    for (int kb = wave * kw; kb < (wave + 1) * kw; kb += 32) {
+        const int c = kb + 8 * kq;
+        float e[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) e[x] = 0.0f;
+        for (int s = 0; s < splits; s++) {
+            const float w = wgt[r16][s];
+            const float4 a0 = *(const float4*)(src + (long)s * H * d + c);
+            const float4 a1 = *(const float4*)(src + (long)s * H * d + c + 4);
+            e[0] += w * a0.x; e[1] += w * a0.y; e[2] += w * a0.z; e[3] += w * a0.w;
+            e[4] += w * a1.x; e[5] += w * a1.y; e[6] += w * a1.z; e[7] += w * a1.w;
+        }
+        FT ahi, alo;
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const T hv = (T)e[x];
+            ahi[x] = hv;
+            alo[x] = (T)(e[x] - (float)hv);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const FT bf = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + c));
+            acc[0][j] = mfma16x16x32(ahi, bf, acc[0][j]);
+            acc[1][j] = mfma16x16x32(alo, bf, acc[1][j]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc_s[wave][a * 16 + 4 * kq + r][j * 16 + r16] = acc[a][j][r];
+    __syncthreads();
+    for (int e = tid; e < 16 * 64; e += 256) {
+        const int ti = e >> 6, j = e & 63;
+        if (i0 + ti >= n) continue;
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) v += acc_s[w][ti][j] + acc_s[w][16 + ti][j];
+        out[(long)(i0 + ti) * d + h * 64 + j] = (T)(v + bv[h * 64 + j]);
+    }
+}
+
+int xattn_splits(int n, int Tn) {
+    const int nn = std::max(1, n);
+    const int s = std::max(1, std::min(16, (256 + nn - 1) / nn));
+    return std::min(s, (Tn + 15) / 16);
+}
+
+bool xattn_supported(int d) { return d == 384 || d == 512 || d == 768 || d == 1024 || d == 1280; }
+
+void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
+                        hipStream_t st) {
+    if (n <= 0) return;
+    dim3 grid(d / 64, H, cdiv(n, 64));
+    if (dt == DType::F16)
+        xattn_qproj_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
+    else
+        xattn_qproj_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
+}
+
+template <typename T>
+static void launch_step_t(const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits, float thr,
+                          float* opart, float* ml, hipStream_t st) {
+    dim3 grid(splits, n);
+#define WM_XSTEP(NW_, CT_) \
+    xattn_step_kernel<T, NW_, CT_><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml)
+    switch (d) {
+        case 384: WM_XSTEP(4, 3); break;
+        case 512: WM_XSTEP(8, 2); break;
+        case 768: WM_XSTEP(8, 3); break;
+        case 1024: WM_XSTEP(8, 4); break;
+        case 1280: WM_XSTEP(8, 5); break;
+        default: fprintf(stderr, "whisper_mi355x: direct cross attention needs d in {384,512,768,1024,1280}\n"); abort();
+    }
+#undef WM_XSTEP
+}
+
+void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
+                       float thr, float* opart, float* ml, hipStream_t st) {
+    if (n <= 0) return;
+    if (splits < 1 || splits > 16 || splits > (Tn + 15) / 16) {
+        fprintf(stderr, "whisper_mi355x: bad split count %d\n", splits);
+        abort();
+    }
+    if (dt == DType::F16) launch_step_t<half_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
+    else launch_step_t<bf16_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
+}
+
+void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
+                          int d, int H, void* out, hipStream_t st) {
+    if (n <= 0) return;
+    if (splits > 16 || d % 128) { fprintf(stderr, "whisper_mi355x: combine shape not supported\n"); abort(); }
+    dim3 grid(H, cdiv(n, 16));
+    if (dt == DType::F16)
+        xattn_combine_kernel<half_t><<<grid, 256, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
+    else
+        xattn_combine_kernel<bf16_t><<<grid, 256, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
+}
+
+}  // namespace wm

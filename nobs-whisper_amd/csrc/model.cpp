@@ -314,6 +314,34 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     if (!ok) { munmap(map, fsize); return false; }
     mat(&W.wkv_cross, xkv, (long)2 * Ld * d, d, xrows, false, 0);
     vecf(&W.bkv_cross, xkvb, xbn);
+    {
+        const char* e = getenv("WHISPER_MI355X_CROSS");
+        c->cross_direct = xattn_supported(d) && hp.n_text_head * 64 == d && !(e && strcmp(e, "cache") == 0);
+    }
+    if (c->cross_direct) {
+        // cross K weights per head, transposed: wkT[l][h][c][j] = Wk_l[h*64 + j][c], the B operand of
+        // the Q' projection Q'_h = s * Wk_h^T q_h (kernels/xattn.hip)
+        const int H = hp.n_text_head;
+        std::vector<char> b((size_t)Ld * H * d * 64 * esz);
+        uint16_t* o = (uint16_t*)b.data();
+        for (int l = 0; l < Ld; l++) {
+            const TensorRef* t = xkv[2 * l];
+            for (int h = 0; h < H; h++)
+                for (int j = 0; j < 64; j++)
+                    for (int k = 0; k < d; k++) {
+                        const size_t src = (size_t)(h * 64 + j) * d + k;
+                        uint16_t out;
+                        if (t->type == 1 && dt == DType::F16) memcpy(&out, t->data + 2 * src, 2);
+                        else {
+                            const float f = elem(*t, src);
+                            if (dt == DType::F16) { _Float16 hf = (_Float16)f; memcpy(&out, &hf, 2); }
+                            else out = f2bf(f);
+                        }
+                        o[(((size_t)l * H + h) * d + k) * 64 + j] = out;
+                    }
+        }
+        A.add(&W.wkT, std::move(b));
+    }
     // mel tables (identical libm expressions to whisper.cpp's whisper_global_cache) + filters^T
     {
         std::vector<char> b(3 * 400 * 4);
