@@ -65,46 +65,52 @@ __device__ __forceinline__ v4s ds_read_tr(unsigned lds_addr) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---- Q' projection -----------------------------------------------------------------------------
-// grid (d/64, H, cdiv(n, 64)), 256 threads: wave w = tokens [z*64 + 16w, +16) x 64 columns.
+// grid (cdiv(d, 256), H, cdiv(n, 64)), 256 threads: wave w = columns [256x + 64w, +64) x 64 tokens,
+// K = 64. Swapped product C^T[c][tok] = Wk_h^T[c][:] . q_h[tok][:]: a lane holds 4 consecutive
+// columns of one token, stored as one 8-byte hi and one 8-byte lo write.
 template <typename T>
 __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ q, const T* __restrict__ wkt, int n, int d,
                                                           int H, float scale, T* __restrict__ qx) {
     typedef typename Frag<T>::type FT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int c0 = blockIdx.x * 64, h = blockIdx.y;
-    const int i0 = blockIdx.z * 64 + wave * 16;
-    if (i0 >= n) return;  // wave-uniform
+    const int c0 = blockIdx.x * 256 + wave * 64, h = blockIdx.y, i0 = blockIdx.z * 64;
+    if (c0 >= d) return;  // wave-uniform
     const u32x4 zero = {0, 0, 0, 0};
-    const int ia = i0 + (lane & 15);
-    FT af[2];
+    FT af[4][2], bq[4][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ks++)
-        af[ks] = __builtin_bit_cast(FT, ia < n ? *(const u32x4*)(q + (long)ia * d + h * 64 + ks * 32 + 8 * (lane >> 4)) : zero);
-    f32x4 acc[4];
+    for (int mt = 0; mt < 4; mt++) {
+        const int c = c0 + mt * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int c = c0 + j * 16 + (lane & 15);
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-            const FT bf = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + c) * 64 + ks * 32 + 8 * (lane >> 4)));
-            acc[j] = mfma16x16x32(af[ks], bf, acc[j]);
-        }
+        for (int ks = 0; ks < 2; ks++)
+            af[mt][ks] = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + c) * 64 + ks * 32 + 8 * (lane >> 4)));
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int c = c0 + j * 16 + (lane & 15);
+    for (int nt = 0; nt < 4; nt++) {
+        const int i = i0 + nt * 16 + (lane & 15);
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int i = i0 + 4 * (lane >> 4) + r;
+        for (int ks = 0; ks < 2; ks++)
+            bq[nt][ks] = __builtin_bit_cast(FT, i < n ? *(const u32x4*)(q + (long)i * d + h * 64 + ks * 32 + 8 * (lane >> 4)) : zero);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 4; nt++) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[mt][ks], bq[nt][ks], acc);
+            const int i = i0 + nt * 16 + (lane & 15);
             if (i >= n) continue;
-            const float v = acc[j][r] * scale;
-            const T hi = (T)v;
-            const T lo = (T)(v - (float)hi);
-            qx[((long)i * 2 * H + h) * d + c] = hi;
-            qx[((long)i * 2 * H + H + h) * d + c] = lo;
+            const int c = c0 + mt * 16 + 4 * (lane >> 4);
+            T hi[4], lo[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float v = acc[r] * scale;
+                hi[r] = (T)v;
+                lo[r] = (T)(v - (float)hi[r]);
+            }
+            *(uint2*)(qx + ((long)i * 2 * H + h) * d + c) = *(const uint2*)hi;
+            *(uint2*)(qx + ((long)i * 2 * H + H + h) * d + c) = *(const uint2*)lo;
         }
-    }
 }
 
 // ---- one pass over E per (clip, split) ------------------------------------------------------------
@@ -315,18 +321,25 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
 }
 
 // ---- merge the splits and apply Wv ---------------------------------------------------------------
-// grid (H, cdiv(n, 16)), 256 threads: wave w sums columns [w*d/4, (w+1)*d/4) for 16 tokens x 64
-// outputs; M = 32 rows (E~ hi for the 16 tokens, then lo), N = 64, K = d/4; waves reduced in LDS.
+// grid (H, cdiv(n, 16)), 512 threads. Phase A (every thread, coalesced 16-byte partial reads): the
+// merged E~ = sum_s w_s O_s / L of 16 tokens x d columns, split into hi / lo rows of an LDS image
+// [32][d] (16-byte chunks XOR-swizzled by row). Phase B: wave w takes the 32-column k-steps
+// w, w+8, ...: M = 32 (hi, lo rows), N = 64 outputs, Wv rows straight from global (L2-shared by the
+// head's token blocks); the 8 waves' partial products are summed through LDS.
 // m is in log2 units (the step kernel scales scores by log2 e).
 template <typename T>
-__global__ void __launch_bounds__(256) xattn_combine_kernel(const float* __restrict__ opart, const float* __restrict__ ml,
+__global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restrict__ opart, const float* __restrict__ ml,
                                                             int splits, const T* __restrict__ wv, const float* __restrict__ bv,
                                                             int n, int d, int H, T* __restrict__ out) {
     typedef typename Frag<T>::type FT;
+    constexpr int DMAX = 1280;
     const int h = blockIdx.x, i0 = blockIdx.y * 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    __shared__ float wgt[16][16];
-    __shared__ float acc_s[4][32][65];
+    __shared__ __attribute__((aligned(16))) char lds[32 * DMAX * 2 + 16 * 16 * 4];
+    T* aimg = (T*)lds;                           // [32][d]: rows 0-15 hi, 16-31 lo
+    float* red = (float*)lds;                    // after phase B: [8 waves][32][64] (reuses aimg)
+    float* wgt = (float*)(lds + 32 * DMAX * 2);  // [16 tokens][16 splits]
+    auto slot_of = [&](int row, int ch) { return row * d + ((ch & ~15) | ((ch & 15) ^ (row & 15))) * 8; };
     if (tid < 16) {
         const int i = i0 + tid;
         if (i < n) {
@@ -336,60 +349,69 @@ __global__ void __launch_bounds__(256) xattn_combine_kernel(const float* __restr
             float L = 0.0f;
             for (int s = 0; s < splits; s++) L += __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * p[(long)s * H * 2 + 1];
             const float inv = 1.0f / L;
-            for (int s = 0; s < splits; s++) wgt[tid][s] = __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * inv;
+            for (int s = 0; s < splits; s++) wgt[tid * 16 + s] = __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * inv;
         } else {
-            for (int s = 0; s < splits; s++) wgt[tid][s] = 0.0f;
+            for (int s = 0; s < splits; s++) wgt[tid * 16 + s] = 0.0f;
         }
     }
     __syncthreads();
+    const int q4 = d / 4;
+#pragma unroll 4
+    for (int e = tid; e < 16 * q4; e += 512) {
+        const int t = e / q4, c = (e - t * q4) * 4;
+        const int i = min(i0 + t, n - 1);
+        const float* src = opart + ((long)i * splits * H + h) * d + c;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < splits; s++) {
+            const float w = wgt[t * 16 + s];
+            const float4 x = *(const float4*)(src + (long)s * H * d);
+            a.x += w * x.x; a.y += w * x.y; a.z += w * x.z; a.w += w * x.w;
+        }
+        const float v[4] = {a.x, a.y, a.z, a.w};
+        T hi[4], lo[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hi[k] = (T)v[k];
+            lo[k] = (T)(v[k] - (float)hi[k]);
+        }
+        const int ch = c >> 3, half = ((c >> 2) & 1) * 4;
+        *(uint2*)(aimg + slot_of(t, ch) + half) = *(const uint2*)hi;
+        *(uint2*)(aimg + slot_of(16 + t, ch) + half) = *(const uint2*)lo;
+    }
+    __syncthreads();
     const int r16 = lane & 15, kq = lane >> 4;
-    const int i = min(i0 + r16, n - 1);
-    const float* src = opart + ((long)i * splits * H + h) * d;
     f32x4 acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[a][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int kw = d / 4;
-    for (int kb = wave * kw; kb < (wave + 1) * kw; kb += 32) {
-        const int c = kb + 8 * kq;
-        float e[8];
+    for (int ks = wave; ks < d / 32; ks += 8) {
+        const int c = ks * 32 + 8 * kq;
+        FT bf[4];
 #pragma unroll
-        for (int x = 0; x < 8; x++) e[x] = 0.0f;
-        for (int s = 0; s < splits; s++) {
-            const float w = wgt[r16][s];
-            const float4 a0 = *(const float4*)(src + (long)s * H * d + c);
-            const float4 a1 = *(const float4*)(src + (long)s * H * d + c + 4);
-            e[0] += w * a0.x; e[1] += w * a0.y; e[2] += w * a0.z; e[3] += w * a0.w;
-            e[4] += w * a1.x; e[5] += w * a1.y; e[6] += w * a1.z; e[7] += w * a1.w;
-        }
-        FT ahi, alo;
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const T hv = (T)e[x];
-            ahi[x] = hv;
-            alo[x] = (T)(e[x] - (float)hv);
-        }
+        for (int j = 0; j < 4; j++) bf[j] = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + c));
+        const FT ahi = *(const FT*)(aimg + slot_of(r16, ks * 4 + kq));
+        const FT alo = *(const FT*)(aimg + slot_of(16 + r16, ks * 4 + kq));
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const FT bf = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + c));
-            acc[0][j] = mfma16x16x32(ahi, bf, acc[0][j]);
-            acc[1][j] = mfma16x16x32(alo, bf, acc[1][j]);
+            acc[0][j] = mfma16x16x32(ahi, bf[j], acc[0][j]);
+            acc[1][j] = mfma16x16x32(alo, bf[j], acc[1][j]);
         }
     }
+    __syncthreads();  // every wave is done with aimg
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) acc_s[wave][a * 16 + 4 * kq + r][j * 16 + r16] = acc[a][j][r];
+            for (int r = 0; r < 4; r++) red[(wave * 32 + a * 16 + 4 * kq + r) * 64 + j * 16 + r16] = acc[a][j][r];
     __syncthreads();
-    for (int e = tid; e < 16 * 64; e += 256) {
+    for (int e = tid; e < 16 * 64; e += 512) {
         const int ti = e >> 6, j = e & 63;
         if (i0 + ti >= n) continue;
         float v = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 4; w++) v += acc_s[w][ti][j] + acc_s[w][16 + ti][j];
+        for (int w = 0; w < 8; w++) v += red[(w * 32 + ti) * 64 + j] + red[(w * 32 + 16 + ti) * 64 + j];
         out[(long)(i0 + ti) * d + h * 64 + j] = (T)(v + bv[h * 64 + j]);
     }
 }
@@ -405,7 +427,7 @@ bool xattn_supported(int d) { return d == 384 || d == 512 || d == 768 || d == 10
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st) {
     if (n <= 0) return;
-    dim3 grid(d / 64, H, cdiv(n, 64));
+    dim3 grid(cdiv(d, 256), H, cdiv(n, 64));
     if (dt == DType::F16)
         xattn_qproj_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
     else
@@ -443,12 +465,12 @@ void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* q
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st) {
     if (n <= 0) return;
-    if (splits > 16 || d % 128) { fprintf(stderr, "whisper_mi355x: combine shape not supported\n"); abort(); }
+    if (splits > 16 || d % 128 || d > 1280) { fprintf(stderr, "whisper_mi355x: combine shape not supported\n"); abort(); }
     dim3 grid(H, cdiv(n, 16));
     if (dt == DType::F16)
-        xattn_combine_kernel<half_t><<<grid, 256, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
+        xattn_combine_kernel<half_t><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
     else
-        xattn_combine_kernel<bf16_t><<<grid, 256, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
+        xattn_combine_kernel<bf16_t><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
 }
 
 }  // namespace wm
