@@ -31,30 +31,34 @@ static hipEvent_t kt_event(whisper_state* s) {
 // is added as an explicit event-record node of the graph: a stream-captured hipEventRecord does
 // not yield a timestamp on replay (hipEventElapsedTime -> invalid handle), an explicit node does
 // (tools/probe/graph_events.hip).
-static void kt_record(whisper_state* s, hipEvent_t e) {
-    if (!s->capture_ev) { WM_CHECK(hipEventRecord(e, s->stream)); return; }
+static void kt_record(whisper_state* s, hipEvent_t e, hipStream_t st) {
+    if (!s->capture_ev) { WM_CHECK(hipEventRecord(e, st)); return; }
     hipStreamCaptureStatus cs;
     unsigned long long id = 0;
     hipGraph_t g = nullptr;
     const hipGraphNode_t* deps = nullptr;
     size_t nd = 0;
-    WM_CHECK(hipStreamGetCaptureInfo_v2(s->stream, &cs, &id, &g, &deps, &nd));
+    WM_CHECK(hipStreamGetCaptureInfo_v2(st, &cs, &id, &g, &deps, &nd));
     hipGraphNode_t node;
     WM_CHECK(hipGraphAddEventRecordNode(&node, g, deps, nd, e));
-    WM_CHECK(hipStreamUpdateCaptureDependencies(s->stream, &node, 1, hipStreamSetCaptureDependencies));
+    WM_CHECK(hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies));
 }
+// Times the launches of its scope on stream `st` (default: the state's stream) when the class is
+// enabled. For K_ATTN_SELF `work` is the share of the step's rows (the bytes grow every step and
+// are filled in when the events are read).
 struct KT {
     whisper_state* s;
     int cls;
     double work;
+    hipStream_t st;
     hipEvent_t a = nullptr;
-    KT(whisper_state* s_, int c, double w) : s(s_), cls(c), work(w) {
-        if ((s->ktime_mask >> c) & 1) { a = kt_event(s); kt_record(s, a); }
+    KT(whisper_state* s_, int c, double w, hipStream_t st_ = nullptr) : s(s_), cls(c), work(w), st(st_ ? st_ : s_->stream) {
+        if ((s->ktime_mask >> c) & 1) { a = kt_event(s); kt_record(s, a, st); }
     }
     ~KT() {
         if (!a) return;
         hipEvent_t b = kt_event(s);
-        kt_record(s, b);
+        kt_record(s, b, st);
         (s->capture_ev ? *s->capture_ev : s->kpending).push_back({cls, a, b, work});
     }
 };
@@ -78,7 +82,7 @@ static void kt_flush_graph(whisper_state* s, const whisper_state::DecGraph& g) {
             continue;
         }
         s->kstat[p.cls].ms += ms;
-        s->kstat[p.cls].work += p.cls == K_ATTN_SELF ? s->cur_self_work : p.work;
+        s->kstat[p.cls].work += p.cls == K_ATTN_SELF ? s->cur_self_work * p.work : p.work;
         s->kstat[p.cls].count++;
     }
 }
@@ -89,7 +93,7 @@ void kt_flush(whisper_state* s) {
         float ms = 0.0f;
         WM_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
         s->kstat[p.cls].ms += ms;
-        s->kstat[p.cls].work += p.work;
+        s->kstat[p.cls].work += p.cls == K_ATTN_SELF ? s->cur_self_work * p.work : p.work;
         s->kstat[p.cls].count++;
         s->kpool.push_back(p.a);
         s->kpool.push_back(p.b);
@@ -98,13 +102,17 @@ void kt_flush(whisper_state* s) {
 }
 // GEMM launch with its algorithmic work: FLOPs for encoder-side GEMMs (MFMA-bound), HBM bytes
 // (weights + activations) for decode-side GEMMs (weight-streaming)
-static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st) {
+static void tgemm_ws(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st, float* ws,
+                     long ws_elems) {
     GemmArgs g = g0;
-    if (cls == K_GEMM_DEC) { g.splitk_ws = s->ws.splitk; g.splitk_ws_elems = s->ws.splitk_elems; }
+    if (cls == K_GEMM_DEC) { g.splitk_ws = ws; g.splitk_ws_elems = ws_elems; }
     const double work = cls == K_GEMM_ENC ? 2.0 * g.M * g.N * g.K
                                           : 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N;
-    KT kt(s, cls, work);
+    KT kt(s, cls, work, st);
     launch_gemm(dt, epi, g, st);
+}
+static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st) {
+    tgemm_ws(s, cls, dt, epi, g0, st, s->ws.splitk, s->ws.splitk_elems);
 }
 
 whisper_state* new_state(Context* c) {
@@ -112,6 +120,9 @@ whisper_state* new_state(Context* c) {
     whisper_state* s = new whisper_state();
     s->ctx = c;
     WM_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    WM_CHECK(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
+    WM_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    WM_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
     return s;
 }
 
@@ -134,6 +145,10 @@ void free_state(whisper_state* s) {
     hipStreamSynchronize(s->stream);
     drop_graphs(s);
     free_ws(s->ws);
+    hipStreamSynchronize(s->stream2);
+    hipEventDestroy(s->ev_fork);
+    hipEventDestroy(s->ev_join);
+    hipStreamDestroy(s->stream2);
     hipStreamDestroy(s->stream);
     delete s;
 }
@@ -192,7 +207,8 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
             // no cross K/V cache up front: decode steps (and short prefills) read E directly
             const int H = hp.n_text_head;
             w.cap_xq = std::max(kXDirectMaxTok * n_jobs, 128);
-            const size_t xo_rows = std::max(w.cap_xq, 512);  // n * xattn_splits(n) <= max(n, 511)
+            // n * xattn_splits(n) <= max(n, 255 + n); two decode row groups at most double that
+            const size_t xo_rows = (size_t)std::max(w.cap_xq, 512) + n_jobs + 512;
             WM_CHECK(hipMalloc(&w.enc, (size_t)n_jobs * T * d * E));
             WM_CHECK(hipMalloc(&w.qx, (size_t)w.cap_xq * 2 * H * d * E));
             WM_CHECK(hipMalloc((void**)&w.xo, xo_rows * H * d * 4));
@@ -396,102 +412,165 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) 
     WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, s->stream));
 }
 
-// the decoder forward over n_tok tokens + logits of n_rows rows; kernels only (graph-capturable).
-// Decode steps (one token per clip, logits for every row, <= 128 rows) take the fused path: every
-// LayerNorm is folded into the embedding or into the split-K reduce of the preceding residual GEMM.
-static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
+// One group of decoder rows on one stream: rows [r0, r0+n) of the token arrays and activations,
+// with its own split-K slab region and cross-attention partials, so that two groups can run at the
+// same time (decode steps).
+struct DecView {
+    int r0, n;
+    hipStream_t st;
+    float* splitk;
+    long splitk_elems;
+    float *xo, *xml;
+};
+
+// The decoder forward over the view's tokens + logits; kernels only (graph-capturable). `fused`
+// (decode steps: one token per clip, logits for every row, <= 128 rows per view): every LayerNorm
+// is folded into the embedding or into the split-K reduce of the preceding residual GEMM.
+// Otherwise (prefill, one view at r0 = 0) logits of n_rows rows (row r = token lrows[r]).
+static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_rows, bool fused, bool xdirect,
+                         double self_share) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
     const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
     const DType dt = c->dt;
     const Weights& W = c->w;
-    hipStream_t st = s->stream;
+    const size_t E = esize(dt);
+    hipStream_t st = v.st;
+    const int n_tok = v.n;
     const int KCLS = K_GEMM_DEC;
     const double kvrow = (double)H * 64 * 2 * 2;  // K and V row bytes of one position, all heads
-    const bool fused = rows_identity && n_rows == n_tok && n_tok <= 128;
+    int* tok = w.tok + v.r0;
+    int* pos = w.pos + v.r0;
+    int* slot = w.slot + v.r0;
+    int* nkv_self = w.nkv_self + v.r0;
+    int* nkv_cross = w.nkv_cross + v.r0;
+    float* dx = w.dx + (size_t)v.r0 * d;
+    void* dh = (char*)w.dh + (size_t)v.r0 * d * E;
+    void* dq = (char*)w.dq + (size_t)v.r0 * d * E;
+    void* datt = (char*)w.datt + (size_t)v.r0 * d * E;
+    void* dff = (char*)w.dff + (size_t)v.r0 * 4 * d * E;
+    void* qx = w.qx ? (void*)((char*)w.qx + (size_t)v.r0 * 2 * H * d * E) : nullptr;
+    auto gemm = [&](int cls, int epi, const GemmArgs& g) { tgemm_ws(s, cls, dt, epi, g, st, v.splitk, v.splitk_elems); };
     auto resid = [&](const void* A, int K, const void* Wt, const float* bias, const float* lnw, const float* lnb) {
-        GemmArgs g = gemm_plain(A, n_tok, K, Wt, d, bias, w.dx, d);
-        if (fused) { g.ln_w = lnw; g.ln_b = lnb; g.ln_out = w.dh; }
-        tgemm(s, KCLS, dt, EPI_RESID, g, st);
-        if (!fused && lnw) launch_layernorm(dt, w.dx, nullptr, n_tok, d, lnw, lnb, w.dh, st);
+        GemmArgs g = gemm_plain(A, n_tok, K, Wt, d, bias, dx, d);
+        if (fused) { g.ln_w = lnw; g.ln_b = lnb; g.ln_out = dh; }
+        gemm(KCLS, EPI_RESID, g);
+        if (!fused && lnw) launch_layernorm(dt, dx, nullptr, n_tok, d, lnw, lnb, dh, st);
     };
-    if (fused) launch_embed_ln(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, W.dec[0].ln1_w, W.dec[0].ln1_b, w.dh, st);
+    if (fused) launch_embed_ln(dt, W.tok_emb, W.pos_d, tok, pos, n_tok, d, dx, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
     else {
-        launch_embed(dt, W.tok_emb, W.pos_d, w.tok, w.pos, n_tok, d, w.dx, st);
-        launch_layernorm(dt, w.dx, nullptr, n_tok, d, W.dec[0].ln1_w, W.dec[0].ln1_b, w.dh, st);
+        launch_embed(dt, W.tok_emb, W.pos_d, tok, pos, n_tok, d, dx, st);
+        launch_layernorm(dt, dx, nullptr, n_tok, d, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
     }
-    // decode steps: the QKV and cross-Q projections leave split-K partial sums that the attention
-    // kernels reduce in their prologue (no separate reduce launch)
+    // decode steps: the QKV (and, cache mode, cross-Q) projections leave split-K partial sums that
+    // the attention kernels reduce in their prologue (no separate reduce launch)
     auto partials = [&](const void* A, const void* Wt, int N, const float* bias, float scale) -> DecSlabs {
         GemmArgs g = gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N);
-        g.splitk_ws = w.splitk;
-        g.splitk_ws_elems = w.splitk_elems;
-        KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N);
+        g.splitk_ws = v.splitk;
+        g.splitk_ws_elems = v.splitk_elems;
+        KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
         const int splits = launch_gemm_partials(dt, g, st);
         if (splits <= 0) { fprintf(stderr, "whisper_mi355x: decode partials GEMM not applicable\n"); abort(); }
-        return DecSlabs{w.splitk, splits, (long)n_tok * N, N, bias, scale};
+        return DecSlabs{v.splitk, splits, (long)n_tok * N, N, bias, scale};
     };
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
         if (fused) {
-            const DecSlabs sl = partials(w.dh, Lw.wqkv, 3 * d, Lw.bqkv, c->k_scale);
-            KT kt(s, K_ATTN_SELF, s->cur_self_work);
-            launch_attn_self_step(dt, sl, w.self, w.slot, w.pos, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, st);
+            const DecSlabs sl = partials(dh, Lw.wqkv, 3 * d, Lw.bqkv, c->k_scale);
+            KT kt(s, K_ATTN_SELF, self_share, st);
+            launch_attn_self_step(dt, sl, w.self, slot, pos, n_tok, L, l, H, hp.n_text_ctx, d, datt, st);
         } else {
-            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wqkv, 3 * d, Lw.bqkv, w.dq, d);
+            GemmArgs g = gemm_plain(dh, n_tok, d, Lw.wqkv, 3 * d, Lw.bqkv, dq, d);
             g.scale = c->k_scale;
-            g.cache = w.self; g.row_slot = w.slot; g.row_pos = w.pos; g.L = L; g.layer = l; g.H = H;
+            g.cache = w.self; g.row_slot = slot; g.row_pos = pos; g.L = L; g.layer = l; g.H = H;
             g.ctx = hp.n_text_ctx; g.d = d;
-            tgemm(s, KCLS, dt, EPI_QKV_DEC, g, st);
-            KT kt(s, K_ATTN_SELF, s->cur_self_work);
-            launch_attn_decode(dt, w.dq, d, w.self, w.slot, w.nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, w.datt, 0, st);
+            gemm(KCLS, EPI_QKV_DEC, g);
+            KT kt(s, K_ATTN_SELF, self_share, st);
+            launch_attn_decode(dt, dq, d, w.self, slot, nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, datt, 0, st);
         }
-        resid(w.datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
+        resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
         if (xdirect) {
             // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
             // -> one pass over E per clip -> split merge + Wv
-            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
+            GemmArgs g = gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
-            tgemm(s, KCLS, dt, EPI_STORE, g, st);
+            gemm(KCLS, EPI_STORE, g);
             const int Ta = hp.n_audio_ctx, S = xattn_splits(n_tok, Ta);
             {
-                KT kt(s, KCLS, 2.0 * d * d + 2.0 * n_tok * d + 4.0 * n_tok * H * d);
-                launch_xattn_qproj(dt, w.dq, (const char*)W.wkT + (size_t)l * H * d * 64 * 2, n_tok, d, H, c->k_scale, w.qx, st);
+                KT kt(s, KCLS, 2.0 * d * d + 2.0 * n_tok * d + 4.0 * n_tok * H * d, st);
+                launch_xattn_qproj(dt, dq, (const char*)W.wkT + (size_t)l * H * d * 64 * 2, n_tok, d, H, c->k_scale, qx, st);
             }
             {
                 // the roofline class holds decode steps only (E bytes read once per clip and layer)
-                KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2);
-                launch_xattn_step(dt, w.enc, w.slot, w.qx, n_tok, Ta, d, S, kXattnThr, w.xo, w.xml, st);
+                KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2, st);
+                launch_xattn_step(dt, w.enc, slot, qx, n_tok, Ta, d, S, kXattnThr, v.xo, v.xml, st);
             }
             {
-                KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d);
-                launch_xattn_combine(dt, w.xo, w.xml, S, (const char*)W.wkv_cross + (size_t)(2 * l + 1) * d * d * 2,
-                                     W.bkv_cross + (size_t)(2 * l + 1) * d, n_tok, d, H, w.datt, st);
+                KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d, st);
+                launch_xattn_combine(dt, v.xo, v.xml, S, (const char*)W.wkv_cross + (size_t)(2 * l + 1) * d * d * 2,
+                                     W.bkv_cross + (size_t)(2 * l + 1) * d, n_tok, d, H, datt, st);
             }
         } else if (fused) {
-            const DecSlabs sl = partials(w.dh, Lw.wxq, d, Lw.bxq, c->k_scale);
-            KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow);  // the class holds decode steps only
-            launch_attn_cross_step(dt, sl, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, st);
+            const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale);
+            KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow, st);  // the class holds decode steps only
+            launch_attn_cross_step(dt, sl, w.cross, slot, nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, datt, st);
         } else {
-            GemmArgs g = gemm_plain(w.dh, n_tok, d, Lw.wxq, d, Lw.bxq, w.dq, d);
+            GemmArgs g = gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
-            tgemm(s, KCLS, dt, EPI_STORE, g, st);
-            KT kt(s, K_OTHER, (double)n_tok * hp.n_audio_ctx * kvrow);
-            launch_attn_decode(dt, w.dq, d, w.cross, w.slot, w.nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, w.datt, 2, st);
+            gemm(KCLS, EPI_STORE, g);
+            KT kt(s, K_OTHER, (double)n_tok * hp.n_audio_ctx * kvrow, st);
+            launch_attn_decode(dt, dq, d, w.cross, slot, nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, datt, 2, st);
         }
-        resid(w.datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
-        tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, w.dff, 4 * d), st);
-        if (l + 1 < L) resid(w.dff, 4 * d, Lw.w2, Lw.b2, W.dec[l + 1].ln1_w, W.dec[l + 1].ln1_b);
-        else if (fused) resid(w.dff, 4 * d, Lw.w2, Lw.b2, W.lnd_w, W.lnd_b);  // dh = final LN of every row
-        else resid(w.dff, 4 * d, Lw.w2, Lw.b2, nullptr, nullptr);
+        resid(datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
+        gemm(KCLS, EPI_GELU, gemm_plain(dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d));
+        if (l + 1 < L) resid(dff, 4 * d, Lw.w2, Lw.b2, W.dec[l + 1].ln1_w, W.dec[l + 1].ln1_b);
+        else if (fused) resid(dff, 4 * d, Lw.w2, Lw.b2, W.lnd_w, W.lnd_b);  // dh = final LN of every row
+        else resid(dff, 4 * d, Lw.w2, Lw.b2, nullptr, nullptr);
     }
     if (fused) {
-        tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.dh, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+        gemm(KCLS, EPI_F32, gemm_plain(dh, n_tok, d, W.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V));
     } else {
         launch_layernorm(dt, w.dx, w.lrows, n_rows, d, W.lnd_w, W.lnd_b, w.lrow, st);
-        tgemm(s, KCLS, dt, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V), st);
+        gemm(KCLS, EPI_F32, gemm_plain(w.lrow, n_rows, d, W.tok_emb, V, nullptr, w.logits, V));
     }
 }
+
+// Decode steps of >= 32 clips run as two row groups, one per stream, forked from and joined back
+// into the state's stream (captured into the step's hipGraph as two independent branches): each
+// group's chain of small, latency-bound GEMM/attention launches overlaps the other's.
+// WHISPER_MI355X_DEC_STREAMS=1 keeps one group.
+static int dec_groups(int n_tok) {
+    static const int g = [] {
+        const char* e = getenv("WHISPER_MI355X_DEC_STREAMS");
+        return e ? atoi(e) : 2;
+    }();
+    return (g >= 2 && n_tok >= 32) ? 2 : 1;
+}
+
+static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
+    Workspace& w = s->ws;
+    const int groups = rows_identity && n_rows == n_tok ? dec_groups(n_tok) : 1;
+    const bool fused = rows_identity && n_rows == n_tok && cdiv(n_tok, groups) <= 128;
+    if (groups == 1 || !fused) {
+        const DecView v{0, n_tok, s->stream, w.splitk, w.splitk_elems, w.xo, w.xml};
+        decoder_rows(c, s, v, n_rows, fused, xdirect, 1.0);
+        return;
+    }
+    const int H = c->hp.n_text_head, d = c->hp.n_text_state;
+    const int na = (n_tok + 1) / 2, nb = n_tok - na;
+    const long half = w.splitk_elems / 2;
+    const long xoff = xdirect ? (long)na * xattn_splits(na, c->hp.n_audio_ctx) : 0;
+    const DecView a{0, na, s->stream, w.splitk, half, w.xo, w.xml};
+    const DecView b{na, nb, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
+                    w.xml ? w.xml + xoff * H * 2 : nullptr};
+    WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
+    WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
+    decoder_rows(c, s, a, na, true, xdirect, (double)na / n_tok);
+    decoder_rows(c, s, b, nb, true, xdirect, (double)nb / n_tok);
+    WM_CHECK(hipEventRecord(s->ev_join, s->stream2));
+    WM_CHECK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
+}
+
 
 // Cross K/V of the given slots (all decoder layers, one GEMM per clip) into the cache, for slots
 // whose cache is stale: direct mode computes it only for prompts too long for the direct prefill.

@@ -146,6 +146,9 @@ struct KStat { double ms = 0, work = 0; long count = 0; };
 struct whisper_state {
     wm::Context* ctx = nullptr;
     hipStream_t stream = nullptr;
+    // second stream + fork/join events: decode steps run their rows as two groups concurrently
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     wm::Workspace ws;
     // whisper.h single-clip results (job 0 of the last call) + batch results
     std::vector<std::vector<wm::Segment>> results;
