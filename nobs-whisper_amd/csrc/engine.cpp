@@ -535,14 +535,15 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     }
 }
 
-// Decode steps of >= 32 clips run as two row groups, one per stream, forked from and joined back
-// into the state's stream (captured into the step's hipGraph as two independent branches): each
-// group's chain of small, latency-bound GEMM/attention launches overlaps the other's.
-// WHISPER_MI355X_DEC_STREAMS=1 keeps one group.
+// WHISPER_MI355X_DEC_STREAMS=2: decode steps of >= 32 clips run as two row groups, one per stream,
+// forked from and joined back into the state's stream (two independent branches of the step's
+// hipGraph), so that each group's chain of small latency-bound launches could overlap the other's.
+// Off by default: measured slower on large-v3 at 128 clips (2360-2392 vs 2729-2740 audio-s/s;
+// the cross-attention pass at 64 clips per group reads E at 3.6 instead of 4.7 TB/s).
 static int dec_groups(int n_tok) {
     static const int g = [] {
         const char* e = getenv("WHISPER_MI355X_DEC_STREAMS");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : 1;
     }();
     return (g >= 2 && n_tok >= 32) ? 2 : 1;
 }

@@ -354,6 +354,20 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
             for (int s = 0; s < splits; s++) wgt[tid * 16 + s] = 0.0f;
         }
     }
+    // Wv fragments of this wave's k-steps (w, w+8, ...; d <= 1280 gives at most 5), loaded before
+    // phase A so their L2 latency overlaps the partial-O reads
+    constexpr int KMAX = DMAX / 256;
+    const int r16 = lane & 15, kq = lane >> 4;
+    FT bfp[KMAX][4];
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+        const int ks = wave + 8 * k;
+        if (ks < d / 32) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                bfp[k][j] = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + ks * 32 + 8 * kq));
+        }
+    }
     __syncthreads();
     const int q4 = d / 4;
 #pragma unroll 4
@@ -379,23 +393,21 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         *(uint2*)(aimg + slot_of(16 + t, ch) + half) = *(const uint2*)lo;
     }
     __syncthreads();
-    const int r16 = lane & 15, kq = lane >> 4;
     f32x4 acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[a][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int ks = wave; ks < d / 32; ks += 8) {
-        const int c = ks * 32 + 8 * kq;
-        FT bf[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) bf[j] = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + c));
+    for (int k = 0; k < KMAX; k++) {
+        const int ks = wave + 8 * k;
+        if (ks >= d / 32) break;  // wave-uniform
         const FT ahi = *(const FT*)(aimg + slot_of(r16, ks * 4 + kq));
         const FT alo = *(const FT*)(aimg + slot_of(16 + r16, ks * 4 + kq));
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            acc[0][j] = mfma16x16x32(ahi, bf[j], acc[0][j]);
-            acc[1][j] = mfma16x16x32(alo, bf[j], acc[1][j]);
+            acc[0][j] = mfma16x16x32(ahi, bfp[k][j], acc[0][j]);
+            acc[1][j] = mfma16x16x32(alo, bfp[k][j], acc[1][j]);
         }
     }
     __syncthreads();  // every wave is done with aimg
