@@ -96,21 +96,22 @@ K_SYMBOL = {"gemm_encoder": r"gemm256_kernel", "attn_encoder": r"attn_enc2_kerne
             "attn_cross_decode": r"xattn_step_kernel"}
 
 
-def pmc_traffic(kernel_class: str):
-    """Launch-weighted HBM bytes per launch of the class's kernel from the newest committed
-    profiles/*_pmc_traffic.json (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE), or
-    None when no PMC pass covers it."""
+def pmc_traffic(kernel_class: str, grid_threads: int | None = None):
+    """Launch-weighted HBM bytes per launch of the class's kernel (restricted to launches of
+    `grid_threads` threads when given) from the newest committed profiles/*_pmc_traffic.json
+    (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE), or None when no PMC pass covers it."""
     import glob
     import re
     pat = K_SYMBOL.get(kernel_class)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
     if not pat or not files:
         return None, None
     with open(files[-1]) as f:
         data = json.load(f)
     n = tb = 0.0
     for sym, v in data.items():
-        if re.search(pat, sym):
+        name, _, grid = sym.partition("@grid=")
+        if re.search(pat, name) and (grid_threads is None or grid == str(grid_threads)):
             n += v["launches"]
             tb += v["traffic_bytes"] * v["launches"]
     return (tb / n if n else None), os.path.basename(files[-1])
@@ -248,7 +249,10 @@ def main():
             achieved = k_work / (k_ms * 1e-3) / 1e9
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
-        traffic, src = pmc_traffic(K_NAMES[dom])
+        grid = None
+        if K_NAMES[dom] == "attn_cross_decode":  # decode-step launches: splits x clips workgroups of 512
+            grid = max(1, min(16, -(-256 // args.batch))) * args.batch * 512
+        traffic, src = pmc_traffic(K_NAMES[dom], grid)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                         traffic_source=f"profiles/{src}")

@@ -4,7 +4,9 @@ FETCH_SIZE and WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters x 64
 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half the bytes of a wide coalesced
 (16 B/lane) streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
 Infinity-Cache hits are counted by these counters (not excluded).
-Writes profiles/<tag>_pmc_traffic.json: {kernel symbol: {launches, fetch_bytes, write_bytes, traffic_bytes}}.
+Writes profiles/<tag>_pmc_traffic.json: {"<kernel symbol>@grid=<threads>": {launches, fetch_bytes,
+write_bytes, traffic_bytes}} (per launch shape: e.g. the cross-attention kernel's prefill launches
+cover several tokens per clip and must not be averaged with the decode-step launches).
 """
 import csv
 import glob
@@ -26,7 +28,7 @@ def read(counter: str, d: str):
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
-                k = row["Kernel_Name"]
+                k = f'{row["Kernel_Name"]}@grid={row["Grid_Size"]}'  # one entry per launch shape
                 acc[k][0] += 1
                 acc[k][1] += float(row["Counter_Value"])
     return acc
