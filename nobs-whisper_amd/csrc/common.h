@@ -51,17 +51,6 @@ __device__ __forceinline__ f32x16 mfma32x32x16(bfx8 a, bfx8 b, f32x16 c) {
 template <typename T> __device__ __forceinline__ T to_t(float x) { return (T)x; }
 template <typename T> __device__ __forceinline__ float from_t(T x) { return (float)x; }
 
-// whisper.cpp/ggml GELU (GGML_GELU_FP16 path): f16(x) -> f16(gelu_tanh(x)); |x|>=10 shortcuts.
-__device__ __forceinline__ float gelu_ggml(float x) {
-    if (x <= -10.0f) return 0.0f;
-    if (x >= 10.0f) return x;
-    const float h = (float)(half_t)x;
-    const float GELU_COEF_A = 0.044715f;
-    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
-    const float g = 0.5f * h * (1.0f + tanhf(SQRT_2_OVER_PI * h * (1.0f + GELU_COEF_A * h * h)));
-    return (float)(half_t)g;
-}
-
 // Block-wide (256-thread) LayerNorm of one row held in registers: thread t owns columns
 // t + 256*k. ggml_norm arithmetic: double sums, float mean/variance, 1/sqrtf(var + 1e-5), then
 // (v*scale)*w + b with every op separately rounded (explicit _rn intrinsics: no FMA contraction

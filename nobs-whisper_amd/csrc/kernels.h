@@ -26,7 +26,7 @@ void launch_embed_ln(DType dt, const void* tok_emb, const float* pos_emb, const 
 // ---- GEMM (kernels/gemm.hip): C[M][N] = A[M][K] . B[N][K]^T + bias, fused epilogues --------------
 enum Epi : int {
     EPI_STORE = 0,     // T out[orow][n] = (v) * colscale(n)
-    EPI_GELU = 1,      // T out = gelu_ggml(v)
+    EPI_GELU = 1,      // T out = gelu_ggml(v)   (ggml's f16 GELU table)
     EPI_RESID = 2,     // f32 out[orow][n] = v + out[orow][n]            (residual stream, in place)
     EPI_GELU_POS = 3,  // f32 out = gelu_ggml(v) + pos[m % pos_rows][n]   (conv2 + positional emb)
     EPI_F32 = 4,       // f32 out = v                                       (logits)
@@ -52,6 +52,8 @@ struct GemmArgs {
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
+// uploads the f16 GELU table the GELU epilogues read (once per context/device, before any GEMM)
+void init_gelu_table();
 // Decode step (M <= 128, K % 64 == 0): only the split-K partial sums, slabs [splits][M][N] f32 in
 // a.splitk_ws, no epilogue; the consumer reduces them (attention prologues). Returns the split
 // count, or 0 when the shape/workspace does not allow it (the caller then uses launch_gemm).

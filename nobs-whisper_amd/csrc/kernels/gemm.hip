@@ -21,10 +21,42 @@
 #include "../kernels.h"
 
 #include <algorithm>
+#include <cmath>
+#include <vector>
 
 namespace wm {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ggml's GELU is a table over f16 inputs (GGML_GELU_FP16, built with the host's tanhf at ggml
+// init): the same table, built the same way on the host once per context and uploaded, then one
+// L2-resident 2-byte gather per output in the epilogues (bit-exact to the oracle's
+// oracle/oracle_whisper.cpp:253 gelu_ggml; a device tanhf formula is not, and costs ~30 % of the
+// FC1 GEMM).
+__device__ uint16_t g_gelu_tab[65536];
+
+void init_gelu_table() {
+    static std::vector<uint16_t> tab;
+    if (tab.empty()) {
+        tab.resize(65536);
+        const float GELU_COEF_A = 0.044715f;
+        const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+        for (int i = 0; i < 65536; i++) {
+            const uint16_t u = (uint16_t)i;
+            const float x = (float)__builtin_bit_cast(_Float16, u);
+            const float g = 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+            tab[i] = __builtin_bit_cast(uint16_t, (_Float16)g);
+        }
+    }
+    WM_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gelu_tab), tab.data(), tab.size() * sizeof(uint16_t)));
+}
+
+// == gelu_ggml(x), bit for bit
+__device__ __forceinline__ float gelu_tab(float x) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    return (float)__builtin_bit_cast(half_t, g_gelu_tab[__builtin_bit_cast(uint16_t, (half_t)x)]);
+}
 
 template <int EPI, typename T>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float v) {
@@ -35,12 +67,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
         ((T*)g.out)[orow * g.ldo + n] = (T)v;
     } else if constexpr (EPI == EPI_GELU) {
         const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
-        ((T*)g.out)[orow * g.ldo + n] = (T)gelu_ggml(v);
+        ((T*)g.out)[orow * g.ldo + n] = (T)gelu_tab(v);
     } else if constexpr (EPI == EPI_RESID) {
         float* o = (float*)g.out + (long)m * g.ldo + n;
         *o = v + *o;
     } else if constexpr (EPI == EPI_GELU_POS) {
-        ((float*)g.out)[(long)m * g.ldo + n] = gelu_ggml(v) + g.pos[(long)(m % g.pos_rows) * g.N + n];
+        ((float*)g.out)[(long)m * g.ldo + n] = gelu_tab(v) + g.pos[(long)(m % g.pos_rows) * g.N + n];
     } else if constexpr (EPI == EPI_F32) {
         ((float*)g.out)[(long)m * g.ldo + n] = v;
     } else if constexpr (EPI == EPI_CROSSKV) {
@@ -108,7 +140,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             float x = v[k];
-            if constexpr (EPI == EPI_GELU) x = gelu_ggml(x);
+            if constexpr (EPI == EPI_GELU) x = gelu_tab(x);
             else if (sc != 1.0f) x = x * sc;
             o[k] = (T)x;
         }
@@ -129,8 +161,8 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
         for (int k = 0; k < 16; k += 4) {
             const float4 pp = *(const float4*)(p + k);
             float4 x;
-            x.x = gelu_ggml(v[k]) + pp.x; x.y = gelu_ggml(v[k + 1]) + pp.y;
-            x.z = gelu_ggml(v[k + 2]) + pp.z; x.w = gelu_ggml(v[k + 3]) + pp.w;
+            x.x = gelu_tab(v[k]) + pp.x; x.y = gelu_tab(v[k + 1]) + pp.y;
+            x.z = gelu_tab(v[k + 2]) + pp.z; x.w = gelu_tab(v[k + 3]) + pp.w;
             *(float4*)(o + k) = x;
         }
     } else if constexpr (EPI == EPI_F32) {

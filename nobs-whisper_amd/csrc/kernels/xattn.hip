@@ -53,6 +53,8 @@ __device__ __forceinline__ void wait_vm() {
     else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 __device__ __forceinline__ v4s ds_read_tr(unsigned lds_addr) {
@@ -60,6 +62,26 @@ __device__ __forceinline__ v4s ds_read_tr(unsigned lds_addr) {
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr));
     return r;
 }
+// Reductions over the 16 lanes of a row by DPP (quad xor 1, quad xor 2, half-row mirror, row
+// mirror): no LDS round trips, unlike __shfl_xor (ds_bpermute). Every lane gets the same bits (each
+// step adds two values commutatively).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max16(float x) {
+    x = fmaxf(x, dpp_f<0xB1>(x));
+    x = fmaxf(x, dpp_f<0x4E>(x));
+    x = fmaxf(x, dpp_f<0x141>(x));
+    return fmaxf(x, dpp_f<0x140>(x));
+}
+__device__ __forceinline__ float sum16(float x) {
+    x = x + dpp_f<0xB1>(x);
+    x = x + dpp_f<0x4E>(x);
+    x = x + dpp_f<0x141>(x);
+    return x + dpp_f<0x140>(x);
+}
+
 // LDS writes of this wave done, then the workgroup barrier. A raw s_barrier, not __syncthreads():
 // the latter waits vmcnt(0) and would drain the LDS-DMA tiles kept in flight across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -213,13 +235,14 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         for (int j = 0; j < NQ; j++) sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
         {
             const int row = lane & 15;
+            FT ef[CT];  // all reads in flight before the first MFMA
 #pragma unroll
-            for (int kk = 0; kk < CT; kk++) {
-                const int ch = (cw >> 3) + kk * 4 + (lane >> 4);
-                const FT ef = __builtin_bit_cast(FT, st[row * RC + xphys(row, ch)]);
+            for (int kk = 0; kk < CT; kk++)
+                ef[kk] = __builtin_bit_cast(FT, st[row * RC + xphys(row, (cw >> 3) + kk * 4 + (lane >> 4))]);
 #pragma unroll
-                for (int j = 0; j < NQ; j++) sacc[j] = mfma16x16x32(ef, qf[kk][j], sacc[j]);
-            }
+            for (int kk = 0; kk < CT; kk++)
+#pragma unroll
+                for (int j = 0; j < NQ; j++) sacc[j] = mfma16x16x32(ef[kk], qf[kk][j], sacc[j]);
         }
         {
             float* rw = red + wave * 16 * RSR;
@@ -241,9 +264,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
                 sv += rr[H + h];
             }
             const float s2 = (tb + t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
-            float mx = s2;
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            const float mx = max16(s2);
             float alpha = 1.0f;
             if (mx > m_run + thr) {  // first tile (m_run = -inf) or the max moved by more than thr
                 alpha = __builtin_amdgcn_exp2f(m_run - mx);
@@ -251,24 +272,19 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
                 flag[t & 1] = 1;
             }
             const T pt = (T)__builtin_amdgcn_exp2f(s2 - m_run);
-            float ps = (float)pt;
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) ps += __shfl_xor(ps, o);
-            l_run = l_run * alpha + ps;
+            l_run = l_run * alpha + sum16((float)pt);
             pimg[h * 16 + r] = pt;
             if (r == 0) alph[h] = alpha;
         }
         if (tid == 0) flag[(t + 1) & 1] = 0;  // last read in tile t-1's P.V, before B1
         lds_barrier();  // B3: P, alpha and the flag in LDS
 
-        // O^T[cols][heads] += E^T . P^T  (every lane active: the transposed reads need EXEC = all ones)
-        if (flag[t & 1]) {
-            const float al = alph[lane & 31];
-#pragma unroll
-            for (int k = 0; k < CT; k++)
-#pragma unroll
-                for (int r = 0; r < 16; r++) oacc[k][r] *= al;
-        }
+        // O^T[cols][heads] += E^T . P^T  (every lane active: the transposed reads need EXEC = all ones).
+        // E^T fragments by inline-asm ds_read_b64_tr_b16: with an LDS-DMA in flight hipcc puts
+        // vmcnt(0) in front of the builtin form (it cannot rule out the DMA writing the bytes it
+        // reads), which would drain the prefetch of tile t+2; the DMA/read ordering here is the
+        // explicit vmcnt + barrier of B1. P, the E^T fragments and the rescale flag are all read
+        // before the one wait.
         FT pf;
         {
             const T* pr = pimg + (lane & 31) * 16 + 4 * hh;
@@ -276,28 +292,30 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             const v4s hi = *(const v4s*)(pr + 8);
             pf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        {
-            // E^T fragments by inline-asm ds_read_b64_tr_b16: with an LDS-DMA in flight hipcc puts
-            // vmcnt(0) in front of the builtin form (it cannot rule out the DMA writing the bytes it
-            // reads), which would drain the prefetch of tile t+2; the DMA/read ordering here is the
-            // explicit vmcnt + barrier of B1.
-            const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-            const int rlo = 4 * hh + tq, rhi = rlo + 8;
-            const unsigned img = (unsigned)(unsigned long)(lds_ptr_t)(const void*)st;
-            v4s lo[CT], hi[CT];
+        const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+        const int rlo = 4 * hh + tq, rhi = rlo + 8;
+        const unsigned img = (unsigned)(unsigned long)(lds_ptr_t)(const void*)st;
+        v4s elo[CT], ehi[CT];
 #pragma unroll
-            for (int k = 0; k < CT; k++) {
-                const int ch = ((cw + k * 32) >> 3) + tg * 2 + (tp >> 1);
-                lo[k] = ds_read_tr(img + rlo * RC * 16 + 16 * xphys(rlo, ch) + 8 * (tp & 1));
-                hi[k] = ds_read_tr(img + rhi * RC * 16 + 16 * xphys(rhi, ch) + 8 * (tp & 1));
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs behind the wait (guide §5.4 rule 18)
+        for (int k = 0; k < CT; k++) {
+            const int ch = ((cw + k * 32) >> 3) + tg * 2 + (tp >> 1);
+            elo[k] = ds_read_tr(img + rlo * RC * 16 + 16 * xphys(rlo, ch) + 8 * (tp & 1));
+            ehi[k] = ds_read_tr(img + rhi * RC * 16 + 16 * xphys(rhi, ch) + 8 * (tp & 1));
+        }
+        const int fl = flag[t & 1];
+        const float al = alph[lane & 31];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs behind the wait (guide §5.4 rule 18)
+        if (fl) {
 #pragma unroll
-            for (int k = 0; k < CT; k++) {
-                const FT ef = __builtin_bit_cast(FT, __builtin_shufflevector(lo[k], hi[k], 0, 1, 2, 3, 4, 5, 6, 7));
-                oacc[k] = mfma32x32x16(ef, pf, oacc[k]);
-            }
+            for (int k = 0; k < CT; k++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) oacc[k][r] *= al;
+        }
+#pragma unroll
+        for (int k = 0; k < CT; k++) {
+            const FT ef = __builtin_bit_cast(FT, __builtin_shufflevector(elo[k], ehi[k], 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[k] = mfma32x32x16(ef, pf, oacc[k]);
         }
     }
 

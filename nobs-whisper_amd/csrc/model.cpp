@@ -368,6 +368,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         total += (it.second.size() + 255) & ~(size_t)255;
     }
     WM_CHECK(hipSetDevice(device));
+    init_gelu_table();
     WM_CHECK(hipMalloc((void**)&c->arena, total));
     c->arena_bytes = total;
     for (size_t i = 0; i < A.items.size(); i++) {

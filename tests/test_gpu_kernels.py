@@ -24,7 +24,7 @@ def _dev(wrs, ctx, arr):
     return p
 
 
-def _run_gemm(wrs, ctx, A, B, bias, variant, reps=1):
+def _run_gemm(wrs, ctx, A, B, bias, variant, reps=1, epi=4):
     L = wrs.lib()
     L.whisper_mi355x_debug_gemm.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_float)]
@@ -32,11 +32,11 @@ def _run_gemm(wrs, ctx, A, B, bias, variant, reps=1):
     M, K = A.shape
     N = B.shape[0]
     pa, pb, pbias = _dev(wrs, ctx, A), _dev(wrs, ctx, B), _dev(wrs, ctx, bias)
-    out = np.zeros((M, N), np.float32)
+    out = np.zeros((M, N), np.float32 if epi in (2, 4) else np.float16)
     po = _dev(wrs, ctx, out)
     L.whisper_mi355x_set_gemm_variant(variant)
     ms = C.c_float()
-    assert L.whisper_mi355x_debug_gemm(ctx.ptr, 4, C.c_void_p(pa), M, K, C.c_void_p(pb), N, C.c_void_p(pbias),
+    assert L.whisper_mi355x_debug_gemm(ctx.ptr, epi, C.c_void_p(pa), M, K, C.c_void_p(pb), N, C.c_void_p(pbias),
                                        C.c_void_p(po), reps, C.byref(ms)) == 0
     L.whisper_mi355x_set_gemm_variant(-1)
     L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(po), out.nbytes, 2)
@@ -96,3 +96,34 @@ def test_gemm_resid_ln_matches_numpy(wrs, ctx, M, N, K):
     yr = (xr - mu) / np.sqrt(var + 1e-5) * w + b
     err = np.abs(y.astype(np.float64) - yr)
     assert (err <= 2e-3 + 2e-3 * np.abs(yr)).all(), f"LN max err {err.max()}"
+
+
+def _gelu_ggml(x):
+    """ggml_vec_gelu_f32 under GGML_GELU_FP16 (the oracle's gelu_ggml, oracle/oracle_whisper.cpp:253):
+    |x| >= 10 shortcuts, else table[f16(x)], the table built with libm's tanhf in f32 arithmetic."""
+    libm = C.CDLL("libm.so.6")
+    libm.tanhf.restype, libm.tanhf.argtypes = C.c_float, [C.c_float]
+    h = np.arange(65536, dtype=np.uint32).astype(np.uint16).view(np.float16).astype(np.float32)
+    f = np.float32
+    with np.errstate(all="ignore"):
+        arg = (f(0.7978845608028654) * h) * (f(1) + (f(0.044715) * h) * h)
+        t = np.array([libm.tanhf(float(v)) for v in arg], np.float32)
+        table = ((f(0.5) * h) * (f(1) + t)).astype(np.float16)
+    g = table[x.astype(np.float16).view(np.uint16)]
+    return np.where(x <= -10, np.float16(0), np.where(x >= 10, x.astype(np.float16), g))
+
+
+@pytest.mark.parametrize("M,N,K", [(3000, 1536, 384), (64, 1536, 384), (1, 5120, 1280)])
+def test_gemm_gelu_epilogue(wrs, ctx, M, N, K):
+    """The GELU epilogue (ggml's f16 GELU table, built on the host and uploaded) against the same
+    GEMM's f32 output through a numpy restatement of that table, bit for bit; the pre-activations
+    straddle the +-10 shortcuts (values in (-10, 10) that round to +-10 in f16 use the table)."""
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((M, K)).astype(np.float16)
+    B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    bias = np.linspace(-12.0, 12.0, N).astype(np.float32)
+    pre, _ = _run_gemm(wrs, ctx, A, B, bias, -1, epi=4)
+    got, _ = _run_gemm(wrs, ctx, A, B, bias, -1, epi=1)
+    ref = _gelu_ggml(pre)
+    same = (got.view(np.uint16) == ref.view(np.uint16)) | (got.astype(np.float32) == ref.astype(np.float32))
+    assert same.all(), f"{(~same).sum()} of {same.size} differ, e.g. pre {pre[~same][:4]} got {got[~same][:4]} ref {ref[~same][:4]}"
