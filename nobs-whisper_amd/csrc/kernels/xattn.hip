@@ -387,19 +387,35 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         }
     }
     __syncthreads();
+    // the partial sums of all NE chunks of a split in flight at once (split order per element kept)
     const int q4 = d / 4;
-#pragma unroll 4
-    for (int e = tid; e < 16 * q4; e += 512) {
+    constexpr int NE = 16 * (DMAX / 4) / 512;
+    float4 a[NE];
+    const float* src[NE];
+#pragma unroll
+    for (int j = 0; j < NE; j++) {
+        a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int e = min(tid + 512 * j, 16 * q4 - 1);
         const int t = e / q4, c = (e - t * q4) * 4;
-        const int i = min(i0 + t, n - 1);
-        const float* src = opart + ((long)i * splits * H + h) * d + c;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int s = 0; s < splits; s++) {
+        src[j] = opart + ((long)min(i0 + t, n - 1) * splits * H + h) * d + c;
+    }
+    for (int s = 0; s < splits; s++) {
+        float4 x[NE];
+#pragma unroll
+        for (int j = 0; j < NE; j++) x[j] = *(const float4*)(src[j] + (long)s * H * d);
+#pragma unroll
+        for (int j = 0; j < NE; j++) {
+            const int t = min(tid + 512 * j, 16 * q4 - 1) / q4;
             const float w = wgt[t * 16 + s];
-            const float4 x = *(const float4*)(src + (long)s * H * d);
-            a.x += w * x.x; a.y += w * x.y; a.z += w * x.z; a.w += w * x.w;
+            a[j].x += w * x[j].x; a[j].y += w * x[j].y; a[j].z += w * x[j].z; a[j].w += w * x[j].w;
         }
-        const float v[4] = {a.x, a.y, a.z, a.w};
+    }
+#pragma unroll
+    for (int j = 0; j < NE; j++) {
+        const int e = tid + 512 * j;
+        if (e >= 16 * q4) break;
+        const int t = e / q4, c = (e - t * q4) * 4;
+        const float v[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
         T hi[4], lo[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {

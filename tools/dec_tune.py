@@ -35,8 +35,8 @@ for M in Ms:
         out = np.zeros((M, N), np.float32)
         ln = np.ones(N, np.float32)
         ptrs = [_dev(wrs, ctx, a) for a in (A, B, bias, out, ln, ln, out)]
-        for v in (0, 1):
-            for sp in (splits_list if v == 1 else [0]):
+        for v in (1,):
+            for sp in splits_list:
                 L.whisper_mi355x_set_gemm_variant(v)
                 L.whisper_mi355x_set_dec_splits(sp)
                 ms = C.c_float()
