@@ -790,11 +790,12 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
     const int nk = cdiv(g.K, 64);
     if (g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
         // decode step (gemm_dec_kernel): split K until the grid has >= 160 workgroups, chunks of
-        // >= 2 K-tiles (>= 5 once there are >= 16 column tiles: 9.6 vs 10.4 us at N = K = 1280,
-        // M = 128) and <= 8 splits (the reduce reads splits x M x N f32)
+        // >= 2 K-tiles and <= 8 splits (the reduce reads splits x M x N f32). (Chunks of >= 5
+        // K-tiles measured faster in isolation, 9.6 vs 10.4 us at N = K = 1280, but not in the
+        // decode step: 82.0 vs 81.6 us of GEMM + reduce per layer.)
         const int tiles = cdiv(g.N, 64);
         int splits = 1;
-        while (tiles * splits < 160 && splits < 8 && (splits + 1) * (tiles >= 16 ? 5 : 2) <= nk) splits++;
+        while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
@@ -882,7 +883,7 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     if (!g.splitk_ws || g.M > 128 || g.K % 64 != 0) return 0;
     const int nk = g.K / 64, tiles = cdiv(g.N, 64);
     int splits = 1;
-    while (tiles * splits < 160 && splits < 8 && (splits + 1) * (tiles >= 16 ? 5 : 2) <= nk) splits++;
+    while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
     if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
     const int kc = cdiv(nk, splits) * 64;
     splits = cdiv(g.K, kc);
