@@ -58,6 +58,31 @@ __device__ __forceinline__ float gelu_tab(float x) {
     return (float)__builtin_bit_cast(half_t, g_gelu_tab[__builtin_bit_cast(uint16_t, (half_t)x)]);
 }
 
+// The same table in LDS for the big GEMMs' epilogues (LDS is free after their main loop): the
+// entries of |h| < 12 only, [0, 0x4A00) positive and [0x4A00, 0x9400) negative f16 bit patterns
+// (inputs in (-10, 10) round to |h| <= 10), 75.8 KB loaded by LDS-DMA per tile. A random 2-byte
+// gather from LDS costs a few LDS cycles per wave; from the global table it is one TA pass per lane.
+typedef __attribute__((address_space(3))) const uint16_t* lds_u16_t;
+constexpr int kGeluLdsEntries = 2 * 0x4A00;
+__device__ __forceinline__ float gelu_ltab(float x, lds_u16_t t) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    const uint16_t u = __builtin_bit_cast(uint16_t, (half_t)x);
+    return (float)__builtin_bit_cast(half_t, t[(u & 0x7FFF) + (u >> 15) * 0x4A00]);
+}
+// stage the LDS table at `dst` (16-byte aligned): 512 threads, 16-byte LDS-DMA pieces
+__device__ __forceinline__ void gelu_ltab_stage(char* dst, int tid) {
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int NCH = kGeluLdsEntries / 8;  // 4736 = 74 x 64
+    static_assert(NCH % 64 == 0, "whole wave pieces");
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int c0 = wave * 64; c0 < NCH; c0 += 512) {
+        const int c = c0 + lane, e = c * 8;
+        const uint16_t* src = g_gelu_tab + (e < 0x4A00 ? e : 0x8000 + (e - 0x4A00));
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + c0 * 16), 16, 0, 0);
+    }
+}
+
 template <int EPI, typename T>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float v) {
     if (g.bias) v = v + g.bias[n];
@@ -96,8 +121,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
 
 // 16 consecutive outputs of row m starting at column n (n % 16 == 0): the same math as
 // `epilogue`, with 16-byte loads/stores whenever the row segment is in bounds and aligned.
-template <int EPI, typename T>
-__device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, float (&v)[16]) {
+template <int EPI, typename T, bool LTAB = false>
+__device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, float (&v)[16], lds_u16_t ltab = nullptr) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     bool vec = n + 16 <= g.N && EPI != EPI_QKV_DEC;
     long base = 0;
@@ -140,7 +165,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             float x = v[k];
-            if constexpr (EPI == EPI_GELU) x = gelu_tab(x);
+            if constexpr (EPI == EPI_GELU) x = LTAB ? gelu_ltab(x, ltab) : gelu_tab(x);
             else if (sc != 1.0f) x = x * sc;
             o[k] = (T)x;
         }
@@ -161,8 +186,13 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
         for (int k = 0; k < 16; k += 4) {
             const float4 pp = *(const float4*)(p + k);
             float4 x;
-            x.x = gelu_tab(v[k]) + pp.x; x.y = gelu_tab(v[k + 1]) + pp.y;
-            x.z = gelu_tab(v[k + 2]) + pp.z; x.w = gelu_tab(v[k + 3]) + pp.w;
+            if constexpr (LTAB) {
+                x.x = gelu_ltab(v[k], ltab) + pp.x; x.y = gelu_ltab(v[k + 1], ltab) + pp.y;
+                x.z = gelu_ltab(v[k + 2], ltab) + pp.z; x.w = gelu_ltab(v[k + 3], ltab) + pp.w;
+            } else {
+                x.x = gelu_tab(v[k]) + pp.x; x.y = gelu_tab(v[k + 1]) + pp.y;
+                x.z = gelu_tab(v[k + 2]) + pp.z; x.w = gelu_tab(v[k + 3]) + pp.w;
+            }
             *(float4*)(o + k) = x;
         }
     } else if constexpr (EPI == EPI_F32) {
@@ -526,6 +556,167 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
     }
 }
 
+// 256x256x64 tiles, 8 waves (2 x 4), each wave 128x64 — the phase-interleaved schedule of the
+// guide's 256^2 8-phase template, restated for this engine's operand layout. A K-tile is four
+// phases, one per C quadrant of the wave (64 rows x 32 columns x K 64 = 16 MFMAs): each phase reads
+// the register subtile it needs (P1: B cols 0-31 + A rows 0-63; P2: B cols 32-63; P3: A rows
+// 64-127; P4: none — A rows 64-127 and B cols 0-31 are still in registers), then a barrier, the
+// LDS wait, the 16 MFMAs, and a second barrier. The two M-halves of the workgroup (wave groups
+// wr = 0, 1; a SIMD holds one wave of each) run one barrier apart, so on every SIMD one wave
+// issues LDS reads and DMA while the other keeps the MFMA pipe busy.
+// Staging (LDS-DMA, 2 buffers x 64 KiB, one K-tile each; buffer = K-tile & 1): the B half-tiles of
+// K-tile kt+2 are issued in P4(kt) (B of buffer kt&1 was last read in P2(kt)), the A half-tiles of
+// K-tile kt+1 in P1(kt) (A of that buffer was last read in P3(kt-1)); both at least two barriers
+// after the last read of the bytes they replace, for either wave group. P4(kt) retires everything
+// of K-tile kt+1 with a counted vmcnt (only the 4 B loads just issued may stay in flight), and the
+// first read of K-tile kt+1 comes one phase later, after a barrier every issuing wave has passed
+// after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
+// slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
+template <typename T, int EPI>
+__global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n) {
+    typedef typename Frag<T>::type FT;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int BM = 256, BK = 64;
+    __shared__ u32x4 lds[2][(BM + 256) * 8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int m0 = (wgid / tiles_n) * BM, n0 = (wgid % tiles_n) * 256;
+    const T* A = (const T*)g.A;
+    const T* B = (const T*)g.B;
+    // DMA sources: half-tile h (rows h*128 .. +127) = 2 pieces of 8 rows x 128 B per wave
+    const T* a_src[2][2];
+    const T* b_src[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int r = h * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const int m = min(m0 + r, g.M - 1);
+            a_src[h][i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 8;
+            const int n = min(n0 + r, g.N - 1);
+            b_src[h][i] = B + (long)n * g.K + c * 8;
+        }
+    auto stage_a = [&](int kt) {
+        u32x4* st = &lds[kt & 1][0];
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
+                                                 (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
+    };
+    auto stage_b = [&](int kt) {
+        u32x4* st = &lds[kt & 1][BM * 8];
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds((const void*)(b_src[h][i] + kt * BK),
+                                                 (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    FT a0[4][2], a1[4][2], b0[2][2], b1[2][2];  // [frag][k-step]
+    auto read_a = [&](int buf, int mq, FT (&af)[4][2]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int row = wm * 128 + (mq * 4 + i) * 16 + (lane & 15), ch = s * 4 + (lane >> 4);
+                af[i][s] = __builtin_bit_cast(FT, lds[buf][row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+    };
+    auto read_b = [&](int buf, int nq, FT (&bf)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int row = wn * 64 + (nq * 2 + j) * 16 + (lane & 15), ch = s * 4 + (lane >> 4);
+                bf[j][s] = __builtin_bit_cast(FT, lds[buf][BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+            }
+    };
+    auto mfma_q = [&](int mq, int nq, const FT (&af)[4][2], const FT (&bf)[2][2]) {
+        asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+#pragma unroll
+                for (int s = 0; s < 2; s++) acc[mq * 4 + i][nq * 2 + j] = mfma16x16x32(af[i][s], bf[j][s], acc[mq * 4 + i][nq * 2 + j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_barrier" ::: "memory");
+    };
+    const int nk = g.K / BK;
+    // prologue: K-tile 0 (A, B), then B of K-tile 1 and A of K-tile 1
+    stage_a(0);
+    stage_b(0);
+    if (nk > 1) { stage_b(1); stage_a(1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+    for (int kt = 0; kt < nk; kt++) {
+        const int buf = kt & 1;
+        // P1
+        read_b(buf, 0, b0);
+        read_a(buf, 0, a0);
+        if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
+        mfma_q(0, 0, a0, b0);
+        // P2
+        read_b(buf, 1, b1);
+        mfma_q(0, 1, a0, b1);
+        // P3
+        read_a(buf, 1, a1);
+        mfma_q(1, 1, a1, b1);
+        // P4: B of K-tile kt+2, then K-tile kt+1 complete (this wave's part)
+        if (kt + 2 < nk) {
+            stage_b(kt + 2);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        mfma_q(1, 0, a1, b0);
+    }
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");  // the barrier counts of both groups match
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int LDW = 68;  // padded f32 row stride of the staging image
+    float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
+    constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
+    char* ltab_g = (char*)&lds[0][0] + 8 * 16 * LDW * 4;  // after the 8 staging images (34816 B)
+    static_assert(8 * 16 * LDW * 4 + kGeluLdsEntries * 2 <= (BM + 256) * 8 * 16 * 2, "GELU table fits");
+    if constexpr (LT) {
+        gelu_ltab_stage(ltab_g, tid);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const lds_u16_t ltab = (lds_u16_t)(const void*)ltab_g;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) stg[((lane >> 4) * 4 + r) * LDW + j * 16 + (lane & 15)] = acc[i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int row = lane >> 2, c0 = (lane & 3) * 16;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            const float4 x = *(const float4*)(stg + row * LDW + c0 + k);
+            v[k] = x.x; v[k + 1] = x.y; v[k + 2] = x.z; v[k + 3] = x.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if (m < g.M && n < g.N) epilogue16<EPI, T, LT>(g, m, n, v, ltab);
+    }
+}
+
 // Decode-step GEMM (M <= 128 active clips): one workgroup = all M rows x 64 columns x one K chunk.
 // The chunk's K-tiles stream through a 4-deep LDS ring filled by LDS-DMA (96 KiB): four tiles are
 // in flight from the start and each consumed slot is refilled at once, so a workgroup pays about
@@ -626,7 +817,9 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         }
 }
 
-int g_gemm_variant = -1;  // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2, 3 same, pipelined
+// debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2, 3 same,
+// pipelined, 4 256^2 phase-interleaved (the auto choice for big GEMMs)
+int g_gemm_variant = -1;
 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
@@ -768,12 +961,13 @@ static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
-    const bool big256 = g_gemm_variant == 2 || g_gemm_variant == 3 ||
+    const bool big256 = g_gemm_variant >= 2 ||
                         (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && big256) {
         const int tn = cdiv(g.N, 256);
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
-        else gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {

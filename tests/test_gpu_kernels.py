@@ -45,10 +45,11 @@ def _run_gemm(wrs, ctx, A, B, bias, variant, reps=1, epi=4):
     return out, ms.value
 
 
-@pytest.mark.parametrize("M,N,K", [(1500 * 2 + 5, 1280, 1280), (3000, 51866, 384), (257, 384, 1536),
+@pytest.mark.parametrize("M,N,K", [(1500 * 2 + 5, 1280, 1280), (3000, 51866, 384), (257, 384, 1536), (2048, 512, 64),
+                                   (1500, 1024, 128), (4096, 1280, 5120),
                                    (32, 1280, 5120), (128, 3840, 1280), (7, 51866, 384),
                                    (100, 1280, 5120), (128, 5120, 1280), (1, 448, 384)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
 def test_gemm_matches_numpy(wrs, ctx, M, N, K, variant):
     rng = np.random.default_rng(M * 7 + N + K)
     A = rng.standard_normal((M, K)).astype(np.float16)
