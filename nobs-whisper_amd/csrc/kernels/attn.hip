@@ -198,13 +198,16 @@ __global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qk
             vv = *(const u32x4*)(src + 2 * d);
         }
     };
-    // transposed-read address (bytes within a V image) for rows r0..r0+3, this lane's dims
+    // transposed-read address (bytes within a V image) for rows r0..r0+3, this lane's dims. Every
+    // r0 used is 4*hh + a multiple of 8, so the swizzle bit ((row >> 1) & 1) is (tq >> 1) & 1 for
+    // all of them: one lane base per dim block, the rest a compile-time offset (ds_read offset field)
     const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-    auto v_addr = [&](int r0, int db) {
-        const int row = r0 + tq;
+    int vbase[2];
+#pragma unroll
+    for (int db = 0; db < 2; db++) {
         const int ch = db * 4 + tg * 2 + (tp >> 1);
-        return row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2)) + 8 * (tp & 1);
-    };
+        vbase[db] = (4 * hh + tq) * 128 + 16 * (ch ^ (((tq >> 1) & 1) << 2)) + 8 * (tp & 1);
+    }
 
     f32x16 oacc[2];
 #pragma unroll
@@ -255,33 +258,44 @@ __global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qk
             for (int r = 0; r < 16; r++) mx = fmaxf(mx, sacc[kb][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32));
         const float m_new = fmaxf(m_run, mx * c);
+        // the running max of no query in the wave moved: alpha = 1 for every lane, skip the rescale
+        const bool moved = __builtin_amdgcn_ballot_w64(m_new != m_run) != 0;
         const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         m_run = m_new;
+        // exponent arguments and row sums two at a time (v_pk_fma_f32 / v_pk_add_f32); the two
+        // partial sums of a lane are added at the end of the tile
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 c2 = {c, c}, nm2 = {-m_new, -m_new};
         FT pf[4];
-        float ls = 0.0f;
+        f2 ls2 = {0.0f, 0.0f};
 #pragma unroll
         for (int kb = 0; kb < 2; kb++)
 #pragma unroll
             for (int sp = 0; sp < 2; sp++)
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][sp * 8 + j], c, -m_new));
-                    ls += p;
-                    pf[kb * 2 + sp][j] = (T)p;
+                for (int j = 0; j < 8; j += 2) {
+                    const f2 x = {sacc[kb][sp * 8 + j], sacc[kb][sp * 8 + j + 1]};
+                    const f2 e = __builtin_elementwise_fma(x, c2, nm2);
+                    const f2 p = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+                    ls2 += p;
+                    pf[kb * 2 + sp][j] = (T)p.x;
+                    pf[kb * 2 + sp][j + 1] = (T)p.y;
                 }
-        l_run = l_run * alpha + ls;
+        l_run = l_run * alpha + (ls2.x + ls2.y);
+        if (moved) {
 #pragma unroll
-        for (int i = 0; i < 2; i++)
+            for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) oacc[i][r] *= alpha;
+                for (int r = 0; r < 16; r++) oacc[i][r] *= alpha;
+        }
         const char* vimg = (const char*)Vs[cur];
 #pragma unroll
         for (int db = 0; db < 2; db++)
 #pragma unroll
             for (int s = 0; s < 4; s++) {
-                const int r0 = (s >> 1) * 32 + (s & 1) * 16 + 4 * hh;
-                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + v_addr(r0, db)));
-                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + v_addr(r0 + 8, db)));
+                const int r0 = (s >> 1) * 32 + (s & 1) * 16;  // + 4 hh, in vbase
+                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + vbase[db] + r0 * 128));
+                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + vbase[db] + (r0 + 8) * 128));
                 const FT vf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
                 oacc[db] = mfma32x32x16(vf, pf[s], oacc[db]);
             }
