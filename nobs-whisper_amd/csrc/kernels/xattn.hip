@@ -147,7 +147,8 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
     constexpr int RC = D / 8;            // 16-byte chunks per E row
     constexpr int NS = 3;                // LDS stages
     constexpr int TILE = 16 * RC;        // u32x4 per 16-row tile
-    constexpr int RSR = 16 * NQ + 4;     // f32 row stride of the score partials (bank spread)
+    constexpr int NH = (H + 15) / 16;    // score column tiles holding the hi columns (0..H-1)
+    constexpr int RSR = 16 * NH + 4;     // f32 row stride of the score partials (bank spread)
     constexpr int STG_B = NS * TILE * 16, RED_B = NW * 16 * RSR * 4, P_B = 32 * 16 * (int)sizeof(T);
     static_assert(RC % 16 == 0, "d must be a multiple of 128");
     static_assert(H * 16 <= NW * 64, "one softmax lane per (head, row)");
@@ -245,11 +246,26 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
                 for (int j = 0; j < NQ; j++) sacc[j] = mfma16x16x32(ef[kk], qf[kk][j], sacc[j]);
         }
         {
+            // hi + lo of every head inside the wave before the cross-wave exchange: the lo column
+            // H+h sits in tile jh + H/16 at lane offset H%16 (or one tile further, 16 lanes back),
+            // constant per tile, so a DPP row shift brings it under its hi column
+            constexpr int J0 = H / 16, D0 = H % 16;
             float* rw = red + wave * 16 * RSR;
 #pragma unroll
-            for (int j = 0; j < NQ; j++)
+            for (int jh = 0; jh < NH; jh++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) rw[(4 * (lane >> 4) + r) * RSR + j * 16 + (lane & 15)] = sacc[j][r];
+                for (int r = 0; r < 4; r++) {
+                    float lo;
+                    if constexpr (D0 == 0) {
+                        lo = sacc[jh + J0][r];
+                    } else {
+                        const float a = dpp_f<0x100 + D0>(sacc[jh + J0][r]);  // lane L <- L + D0
+                        // lane L <- L - (16 - D0); no such tile: those lanes are past the last head
+                        const float b = jh + J0 + 1 < NQ ? dpp_f<0x110 + 16 - D0>(sacc[min(jh + J0 + 1, NQ - 1)][r]) : 0.0f;
+                        lo = (lane & 15) < 16 - D0 ? a : b;
+                    }
+                    rw[(4 * (lane >> 4) + r) * RSR + jh * 16 + (lane & 15)] = sacc[jh][r] + lo;
+                }
         }
         lds_barrier();  // B2: partial scores of every wave in LDS
 
@@ -259,9 +275,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             float sv = 0.0f;
 #pragma unroll
             for (int w = 0; w < NW; w++) {
-                const float* rr = red + (w * 16 + r) * RSR;
-                sv += rr[h];
-                sv += rr[H + h];
+                sv += red[(w * 16 + r) * RSR + h];
             }
             const float s2 = (tb + t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
             const float mx = max16(s2);
