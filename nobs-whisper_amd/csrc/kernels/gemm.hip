@@ -723,7 +723,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
 // one memory latency per four K-tiles. The grid is (N/64) x splits with the partial tile written
 // to the split-K slab (or through the epilogue when the chunk is the whole K). Rows past M are
 // clamped (their outputs are never stored).
-template <typename T, int EPI, bool SPLIT>
+template <typename T, int EPI, bool SPLIT, int AUXB = 0>
 __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const int kc) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
             __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&st[(wave * 4 + i) * 64], 16, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, AUXB);
     };
     for (int t = 0; t < min(nkt, MAXT); t++) issue(t);
     f32x4 acc[4][2];
@@ -945,6 +945,15 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
 
 int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
 static int dec_splits_override() { return g_dec_splits; }
+// decode-step weights are read once per step by one workgroup each: non-temporal LDS-DMA (aux = 2;
+// 3058-3070 vs 3053-3059 audio-s/s). WHISPER_MI355X_DEC_NT=0 restores the default policy (A/B).
+static bool dec_weight_nt() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_DEC_NT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
 
 template <typename T>
 static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st) {
@@ -998,10 +1007,12 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
-                gemm_dec_kernel<T, EPI, false><<<tiles, 256, 0, st>>>(g, kc);
+                if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<tiles, 256, 0, st>>>(g, kc);
+                else gemm_dec_kernel<T, EPI, false><<<tiles, 256, 0, st>>>(g, kc);
                 return;
             }
-            gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            else gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
             } else {
@@ -1082,7 +1093,8 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     const int kc = cdiv(nk, splits) * 64;
     splits = cdiv(g.K, kc);
     if ((long)splits * g.M * g.N > g.splitk_ws_elems) return 0;
-    gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    if (dec_weight_nt()) gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    else gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
     return splits;
 }
 

@@ -1,3 +1,3 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-DEC_M=128 DEC_SPLITS=${DEC_SPLITS:-0,2,3,4,5,6,8,10} timeout -k 10 300 python3 -u tools/dec_tune.py > gpurun_out/dec_tune.log 2>&1
+DEC_M=128 DEC_SPLITS=${DEC_SPLITS:-0,1} timeout -k 10 300 python3 -u tools/dec_tune.py > gpurun_out/dec_tune.log 2>&1
 rc=$?; cat gpurun_out/dec_tune.log; exit $rc

@@ -6,7 +6,7 @@
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
 ARGS="--tokens 4 --steps 1 --warmup 1 --cpu-baseline 0"
-REGEX="${PMC_REGEX:-xattn_step_kernel|gemm256_kernel|attn_enc2_kernel}"
+REGEX="${PMC_REGEX:-xattn_step_kernel|gemm8p_kernel|attn_enc2_kernel}"
 for c in FETCH_SIZE WRITE_SIZE; do
   d="$R/gpurun_out/pmc_$(echo $c | tr A-Z a-z | cut -d_ -f1)"
   timeout -k 10 ${T_PMC:-500} rocprofv3 --pmc $c --kernel-include-regex "$REGEX" --output-format csv -d "$d" -o run \
