@@ -465,7 +465,19 @@ __global__ void __launch_bounds__(256) attn_cross_step_kernel(const DecSlabs sl,
 // and k scaled, rounded to T), appends k, v to the self cache at pos[i] and attends keys
 // [0, pos) from the cache plus the fresh key from registers. Scores: 8 lanes per key row (16 B
 // each), U rows in flight per lane group; softmax and P.V reductions are wave shuffles.
-template <typename T, int HPB>
+// Sums over the 8 lanes of a key row by DPP (quad xor 1, quad xor 2, half-row mirror): the same
+// bits as the xor butterfly, without LDS round trips. NT: the cached K and V rows (read once per
+// step) by non-temporal loads.
+template <int CTRL>
+__device__ __forceinline__ float dpp8_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8(float a) {
+    a += dpp8_f<0xB1>(a);
+    a += dpp8_f<0x4E>(a);
+    return a + dpp8_f<0x141>(a);
+}
+template <typename T, int HPB, bool NT>
 __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs sl, T* __restrict__ cache,
                                                                   const int* __restrict__ slot,
                                                                   const int* __restrict__ pos_arr, int L, int layer,
@@ -512,7 +524,8 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
-            raw[u] = t < pos ? *(const u32x4*)(K + (long)t * 64 + lane8 * 8) : zero;
+            const u32x4* src = (const u32x4*)(K + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -521,9 +534,7 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
             float a = 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-            a += __shfl_xor(a, 1);
-            a += __shfl_xor(a, 2);
-            a += __shfl_xor(a, 4);
+            a = sum8(a);
             if (t < pos) {
                 if (lane8 == 0) sc[w][t] = a;
                 lmax = fmaxf(lmax, a);
@@ -534,9 +545,7 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
         float a = 0.0f;
 #pragma unroll
         for (int e = 0; e < 8; e++) a += qv[e] * ks[w][lane8 * 8 + e];
-        a += __shfl_xor(a, 1);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 4);
+        a = sum8(a);
         if (lane == 0) sc[w][pos] = a;
         lmax = fmaxf(lmax, a);
     }
@@ -561,7 +570,8 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
-            raw[u] = t < pos ? *(const u32x4*)(V + (long)t * 64 + lane8 * 8) : zero;
+            const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -579,7 +589,7 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     }
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-        acc[e] += __shfl_xor(acc[e], 8);
+        acc[e] += dpp8_f<0x128>(acc[e]);  // row_ror:8 = lane ^ 8 within the 16-lane row
         acc[e] += __shfl_xor(acc[e], 16);
         acc[e] += __shfl_xor(acc[e], 32);
     }
@@ -640,8 +650,15 @@ void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int*
     if (n <= 0) return;
     if (ctx > 448) { fprintf(stderr, "whisper_mi355x: self-attention context %d > 448\n", ctx); abort(); }
     const int hpb = H % 4 == 0 ? 4 : H % 2 == 0 ? 2 : 1;
-#define WM_SELF(TT, HB) \
-    attn_self_step_kernel<TT, HB><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
+    // non-temporal K/V reads with WHISPER_MI355X_SELF_NT=1 (A/B: 3048-3053 vs 3050-3057 audio-s/s
+    // with the default policy, so off)
+    static const bool nt = [] {
+        const char* e = getenv("WHISPER_MI355X_SELF_NT");
+        return e && atoi(e) != 0;
+    }();
+#define WM_SELF(TT, HB)                                                                                                     \
+    if (nt) attn_self_step_kernel<TT, HB, true><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out); \
+    else attn_self_step_kernel<TT, HB, false><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
 #define WM_SELF_H(TT) \
     do { if (hpb == 4) WM_SELF(TT, 4); else if (hpb == 2) WM_SELF(TT, 2); else WM_SELF(TT, 1); } while (0)
     if (dt == DType::F16) WM_SELF_H(half_t);
