@@ -78,6 +78,15 @@ WHISPER_API void whisper_mi355x_set_gemm_variant(int variant);
 WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
 /* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
  * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */
+// fp8 (OCP e4m3) GEMM with per-row f32 scales (A per row m, B per row n), then epilogue `epi`;
+// A8 [M][K], B8 [N][K] bytes, K % 128 == 0 (large-v3-turbo fp8 encoder path)
+WHISPER_API int whisper_mi355x_debug_gemm_fp8(struct whisper_context * ctx, int epi, const void * A8,
+                                              const float * a_scale, int M, int K, const void * B8,
+                                              const float * b_scale, int N, const float * bias, void * out,
+                                              int reps, float * ms);
+// q[r][:] = e4m3(x[r][:] / s[r]), s[r] = max|x[r][:]| / 448; x in the context's MFMA type
+WHISPER_API int whisper_mi355x_debug_quant_fp8(struct whisper_context * ctx, const void * x, long rows, int K,
+                                               void * q, float * s);
 WHISPER_API int whisper_mi355x_debug_gemm_ln(struct whisper_context * ctx, const void * A, int M, int K,
                                              const void * B, int N, const float * bias, float * x,
                                              const float * ln_w, const float * ln_b, void * y, int reps, float * ms);

@@ -52,6 +52,14 @@ struct GemmArgs {
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
+// fp8 (OCP e4m3) operands with per-row f32 scales: C = (A8 . B8^T) * a_scale[m] * b_scale[n], then
+// the epilogue (EPI_STORE / EPI_GELU / EPI_RESID); K % 128 == 0, N % 16 == 0. A/B strides in bytes.
+void launch_gemm_fp8(DType dt, int epi, const GemmArgs& a, const float* a_scale, const float* b_scale, hipStream_t st);
+// q[r][:] = e4m3(x[r][:] / s[r]), s[r] = max|x[r][:]| / 448 (x in the MFMA type, K % 8 == 0)
+void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, float* s, hipStream_t st);
+// LayerNorm (f32 residual rows -> LN * w + b) quantized per row to fp8 e4m3: q [M][D] bytes, s [M]
+void launch_layernorm_fp8(const float* x, int M, int D, const float* w, const float* b, void* q, float* s,
+                          hipStream_t st);
 // uploads the f16 GELU table the GELU epilogues read (once per context/device, before any GEMM)
 void init_gelu_table();
 // Decode step (M <= 128, K % 64 == 0): only the split-K partial sums, slabs [splits][M][N] f32 in

@@ -717,6 +717,201 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     }
 }
 
+// fp8 variant of gemm8p_kernel (large-v3-turbo's fp8 weights, BASELINE configs[4]): A and B are
+// OCP e4m3 bytes with one f32 scale per row (A: per token row, from the quantizing LayerNorm;
+// B: per output channel, quantized once at load), C = (A8 . B8^T) * sa[m] * sb[n] then the same
+// epilogues. The MFMA is the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 with every E8M0
+// block scale 127 (= 1.0): the 2x-bf16-rate fp8 path (the non-scaled fp8 MFMA runs at the bf16
+// rate). A K-tile is 128 elements = the same 128 bytes per row as the bf16 kernel's 64, so the
+// LDS image, swizzle, DMA schedule, barriers and counted waits are unchanged; one MFMA per
+// (fragment, K-tile) instead of two, i.e. half the K-tiles for the same MFMA cycles per tile.
+// A lane's 32 operand bytes are the two adjacent 16-byte chunks 2(l>>4), 2(l>>4)+1 of its row,
+// read identically for A and B: whatever k order the instruction assigns inside a lane, both
+// operands use the same one, so the dot product is over all 128 k of the tile.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma_mx8(i32x8 a, i32x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+template <typename T, int EPI>
+__global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const int tiles_n, const float* __restrict__ sa,
+                                                        const float* __restrict__ sb) {
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    constexpr int BM = 256, BK = 128;  // BK in fp8 elements = bytes
+    __shared__ u32x4 lds[2][(BM + 256) * 8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int m0 = (wgid / tiles_n) * BM, n0 = (wgid % tiles_n) * 256;
+    const uint8_t* A = (const uint8_t*)g.A;
+    const uint8_t* B = (const uint8_t*)g.B;
+    const uint8_t* a_src[2][2];
+    const uint8_t* b_src[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int r = h * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const int m = min(m0 + r, g.M - 1);
+            a_src[h][i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 16;
+            const int n = min(n0 + r, g.N - 1);
+            b_src[h][i] = B + (long)n * g.K + c * 16;
+        }
+    auto stage_a = [&](int kt) {
+        u32x4* st = &lds[kt & 1][0];
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
+                                                 (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
+    };
+    auto stage_b = [&](int kt) {
+        u32x4* st = &lds[kt & 1][BM * 8];
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds((const void*)(b_src[h][i] + kt * BK),
+                                                 (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    i32x8 a0[4], a1[4], b0[2], b1[2];
+    auto frag = [&](const u32x4* img, int row) -> i32x8 {
+        const int c0 = 2 * (lane >> 4), sw = (row >> 1) & 7;
+        const u32x4 x = img[row * 8 + (c0 ^ sw)], y = img[row * 8 + ((c0 + 1) ^ sw)];
+        return (i32x8){(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
+    };
+    auto read_a = [&](int buf, int mq, i32x8 (&af)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) af[i] = frag(&lds[buf][0], wm * 128 + (mq * 4 + i) * 16 + (lane & 15));
+    };
+    auto read_b = [&](int buf, int nq, i32x8 (&bf)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) bf[j] = frag(&lds[buf][BM * 8], wn * 64 + (nq * 2 + j) * 16 + (lane & 15));
+    };
+    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2]) {
+        asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_barrier" ::: "memory");
+    };
+    const int nk = g.K / BK;
+    stage_a(0);
+    stage_b(0);
+    if (nk > 1) { stage_b(1); stage_a(1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");
+    for (int kt = 0; kt < nk; kt++) {
+        const int buf = kt & 1;
+        read_b(buf, 0, b0);
+        read_a(buf, 0, a0);
+        if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
+        mfma_q(0, 0, a0, b0);
+        read_b(buf, 1, b1);
+        mfma_q(0, 1, a0, b1);
+        read_a(buf, 1, a1);
+        mfma_q(1, 1, a1, b1);
+        if (kt + 2 < nk) {
+            stage_b(kt + 2);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        mfma_q(1, 0, a1, b0);
+    }
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int LDW = 68;
+    float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
+    constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
+    char* ltab_g = (char*)&lds[0][0] + 8 * 16 * LDW * 4;
+    if constexpr (LT) {
+        gelu_ltab_stage(ltab_g, tid);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const lds_u16_t ltab = (lds_u16_t)(const void*)ltab_g;
+    const int row = lane >> 2, c0 = (lane & 3) * 16;
+    const int nb = min(n0 + wn * 64 + c0, g.N - 16);
+    float bs[16];
+#pragma unroll
+    for (int k = 0; k < 16; k += 4) {
+        const float4 x = *(const float4*)(sb + nb + k);
+        bs[k] = x.x; bs[k + 1] = x.y; bs[k + 2] = x.z; bs[k + 3] = x.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) stg[((lane >> 4) * 4 + r) * LDW + j * 16 + (lane & 15)] = acc[i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k += 4) {
+            const float4 x = *(const float4*)(stg + row * LDW + c0 + k);
+            v[k] = x.x; v[k + 1] = x.y; v[k + 2] = x.z; v[k + 3] = x.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if (m < g.M && n < g.N) {
+            const float am = sa[m];
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = (v[k] * am) * bs[k];
+            epilogue16<EPI, T, LT>(g, m, n, v, ltab);
+        }
+    }
+}
+
+// fp8 e4m3 (OCP) row quantization: q[r][k] = sat(x[r][k] / s[r]), s[r] = max|x[r][:]| / 448
+// (1 for an all-zero row). One wave per row, K % 8 == 0; used for the weights at load time.
+template <typename T>
+__global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const T* __restrict__ x, long rows, int K,
+                                                             uint8_t* __restrict__ q, float* __restrict__ s) {
+    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    const T* xr = x + r * K;
+    float amax = 0.f;
+    for (int k = lane * 8; k < K; k += 512) {
+        const u32x4 w = *(const u32x4*)(xr + k);
+        const T* t = (const T*)&w;
+#pragma unroll
+        for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf((float)t[j]));
+    }
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float sc = amax > 0.f ? amax / 448.f : 1.f, inv = 1.f / sc;
+    if (lane == 0) s[r] = sc;
+    uint8_t* qr = q + r * K;
+    for (int k = lane * 8; k < K; k += 512) {
+        const u32x4 w = *(const u32x4*)(xr + k);
+        const T* t = (const T*)&w;
+        uint32_t lo = 0, hi = 0;
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf((float)t[0] * inv, -448.f), 448.f),
+                                             fminf(fmaxf((float)t[1] * inv, -448.f), 448.f), lo, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf((float)t[2] * inv, -448.f), 448.f),
+                                             fminf(fmaxf((float)t[3] * inv, -448.f), 448.f), lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf((float)t[4] * inv, -448.f), 448.f),
+                                             fminf(fmaxf((float)t[5] * inv, -448.f), 448.f), hi, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf((float)t[6] * inv, -448.f), 448.f),
+                                             fminf(fmaxf((float)t[7] * inv, -448.f), 448.f), hi, true);
+        *(uint2*)(qr + k) = make_uint2(lo, hi);
+    }
+}
+
 // Decode-step GEMM (M <= 128 active clips): one workgroup = all M rows x 64 columns x one K chunk.
 // The chunk's K-tiles stream through a 4-deep LDS ring filled by LDS-DMA (96 KiB): four tiles are
 // in flight from the start and each consumed slot is refilled at once, so a workgroup pays about
@@ -1100,6 +1295,35 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
 
 int launch_gemm_partials(DType dt, const GemmArgs& g, hipStream_t st) {
     return dt == DType::F16 ? launch_partials_t<half_t>(g, st) : launch_partials_t<bf16_t>(g, st);
+}
+
+template <typename T>
+static void launch_mx_t(int epi, const GemmArgs& g, const float* sa, const float* sb, hipStream_t st) {
+    const int tn = cdiv(g.N, 256), grid = tn * cdiv(g.M, 256);
+    switch (epi) {
+        case EPI_STORE: gemm8p_mx_kernel<T, EPI_STORE><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        case EPI_GELU: gemm8p_mx_kernel<T, EPI_GELU><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        case EPI_RESID: gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        default: fprintf(stderr, "whisper_mi355x: fp8 GEMM epilogue %d not supported\n", epi); abort();
+    }
+}
+
+void launch_gemm_fp8(DType dt, int epi, const GemmArgs& g, const float* a_scale, const float* b_scale, hipStream_t st) {
+    if (g.M <= 0 || g.N <= 0) return;
+    if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || !a_scale || !b_scale) {
+        fprintf(stderr, "whisper_mi355x: fp8 gemm shape not supported (N=%d K=%d)\n", g.N, g.K);
+        abort();
+    }
+    if (dt == DType::F16) launch_mx_t<half_t>(epi, g, a_scale, b_scale, st);
+    else launch_mx_t<bf16_t>(epi, g, a_scale, b_scale, st);
+}
+
+void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, float* s, hipStream_t st) {
+    if (rows <= 0) return;
+    if (K % 8 != 0) { fprintf(stderr, "whisper_mi355x: fp8 quantization needs K %% 8 == 0\n"); abort(); }
+    const unsigned grid = (unsigned)((rows + 3) / 4);
+    if (dt == DType::F16) quant_rows_fp8_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)x, rows, K, (uint8_t*)q, s);
+    else quant_rows_fp8_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)x, rows, K, (uint8_t*)q, s);
 }
 
 void launch_gemm(DType dt, int epi, const GemmArgs& g, hipStream_t st) {

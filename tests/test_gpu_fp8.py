@@ -1,0 +1,117 @@
+"""fp8 (OCP e4m3fn) encoder-GEMM path for large-v3-turbo's fp8 weights (BASELINE configs[4]).
+
+Not a whisper.cpp parity path (whisper.cpp has no fp8 weights): the kernels are checked against
+float64 numpy of the SAME fp8 operands, so the only tolerated difference is accumulation:
+|err| <= 1e-4 * sum_k |a_k b_k| * sa * sb + 1e-6 (the block-scaled MFMA's internal sum over a
+128-k block is not sequential f32 accumulation: measured up to ~2.6e-5 of sum |a b|). The row quantizer is checked for the e4m3 round-
+to-nearest bound: |x/s - q| <= half the e4m3 spacing at q's binade (2^-10 below 2^-6).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def e4m3_decode_table():
+    t = np.zeros(256, np.float64)
+    for b in range(256):
+        sgn = -1.0 if b & 0x80 else 1.0
+        e, m = (b >> 3) & 15, b & 7
+        if e == 15 and m == 7:
+            t[b] = np.nan
+        elif e == 0:
+            t[b] = sgn * (m / 8.0) * 2.0 ** -6
+        else:
+            t[b] = sgn * (1.0 + m / 8.0) * 2.0 ** (e - 7)
+    return t
+
+
+DEC = e4m3_decode_table()
+
+
+def e4m3_spacing(v):
+    """Spacing of e4m3 values in the binade of |v| (subnormal spacing below 2^-6)."""
+    a = np.abs(v)
+    e = np.floor(np.log2(np.maximum(a, 2.0 ** -6)))
+    return 2.0 ** (e - 3)
+
+
+@pytest.fixture(scope="module")
+def ctx(wrs, micro_model):
+    c = wrs.WhisperContext(micro_model, dtype=wrs.F16)
+    yield c
+    c.close()
+
+
+def _dev(L, ctx, arr):
+    p = L.whisper_mi355x_dev_alloc(ctx.ptr, arr.nbytes)
+    assert p
+    L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(p), arr.ctypes.data, arr.nbytes, 1)
+    return p
+
+
+def _get(L, ctx, p, like):
+    out = np.empty_like(like)
+    L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(p), out.nbytes, 2)
+    return out
+
+
+@pytest.mark.parametrize("rows,K", [(5, 1280), (256, 5120), (33, 384)])
+def test_quant_rows_fp8(wrs, ctx, rows, K):
+    L = wrs.lib()
+    L.whisper_mi355x_debug_quant_fp8.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_int, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(rows * 31 + K)
+    x = (rng.standard_normal((rows, K)) * rng.uniform(0.01, 30, (rows, 1))).astype(np.float16)
+    x[0, :] = 0  # all-zero row: scale 1
+    px = _dev(L, ctx, x)
+    q0, s0 = np.zeros((rows, K), np.uint8), np.zeros(rows, np.float32)
+    pq, ps = _dev(L, ctx, q0), _dev(L, ctx, s0)
+    assert L.whisper_mi355x_debug_quant_fp8(ctx.ptr, C.c_void_p(px), rows, K, C.c_void_p(pq), C.c_void_p(ps)) == 0
+    q, s = _get(L, ctx, pq, q0), _get(L, ctx, ps, s0)
+    for p in (px, pq, ps):
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    x64 = x.astype(np.float64)
+    amax = np.abs(x64).max(axis=1)
+    exp_s = np.where(amax > 0, (amax / 448.0).astype(np.float32), 1.0)
+    np.testing.assert_allclose(s, exp_s, rtol=1e-6)
+    deq = DEC[q]
+    assert not np.isnan(deq).any()
+    t = x64 / s[:, None].astype(np.float64)
+    assert (np.abs(t - deq) <= 0.5 * e4m3_spacing(deq) + 1e-6 * np.abs(t) + 1e-12).all()
+    assert (np.abs(deq).max(axis=1)[1:] == 448.0).all()  # the row maximum maps to the e4m3 maximum
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 1280, 1280), (512, 3840, 1280), (257, 768, 3072), (1500, 1280, 5120)])
+@pytest.mark.parametrize("epi", [0, 2])
+def test_gemm_fp8_matches_numpy(wrs, ctx, M, N, K, epi):
+    L = wrs.lib()
+    L.whisper_mi355x_debug_gemm_fp8.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                                C.POINTER(C.c_float)]
+    rng = np.random.default_rng(M + 3 * N + 7 * K + epi)
+    ok = np.array([b for b in range(256) if not np.isnan(DEC[b])], np.uint8)
+    A8 = rng.choice(ok, (M, K)).astype(np.uint8)
+    B8 = rng.choice(ok, (N, K)).astype(np.uint8)
+    sa = rng.uniform(0.001, 0.01, M).astype(np.float32)
+    sb = rng.uniform(0.0001, 0.001, N).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    out0 = np.zeros((M, N), np.float32 if epi == 2 else np.float16)
+    ptrs = [_dev(L, ctx, a) for a in (A8, sa, B8, sb, bias, out0)]
+    pa, psa, pb, psb, pbias, po = ptrs
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_gemm_fp8(ctx.ptr, epi, C.c_void_p(pa), C.c_void_p(psa), M, K, C.c_void_p(pb),
+                                           C.c_void_p(psb), N, C.c_void_p(pbias), C.c_void_p(po), 0,
+                                           C.byref(ms)) == 0
+    out = _get(L, ctx, po, out0).astype(np.float64)
+    for p in ptrs:
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    a64, b64 = DEC[A8], DEC[B8]
+    ref = (a64 @ b64.T) * sa[:, None].astype(np.float64) * sb[None, :].astype(np.float64) + bias
+    mag = (np.abs(a64) @ np.abs(b64).T) * sa[:, None] * sb[None, :]
+    bound = 1e-4 * mag + 1e-6
+    if epi == 0:  # f16 output: + half an f16 ulp
+        bound = bound + np.abs(ref) * 2.0 ** -11 + 2.0 ** -24
+    err = np.abs(out - ref)
+    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
