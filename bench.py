@@ -140,7 +140,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--batch", type=int, default=128, help="30 s chunks per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"],
+                    help="fp8: bf16 with the encoder QKV/FC1/FC2 GEMMs on e4m3 weights + activations")
     ap.add_argument("--tokens", type=int, default=128, help="decode tokens per chunk (fixed-work mode)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -170,7 +171,7 @@ def main():
     barrier()
 
     # ---- context: rank 0 loads, the others receive the weight arena over RCCL (xGMI) -------------
-    dtype = wrs.BF16 if args.dtype == "bf16" else wrs.F16
+    dtype = {"bf16": wrs.BF16, "f16": wrs.F16, "fp8": wrs.FP8_ENC}[args.dtype]
     t_load = time.time()
     ctx = wrs.WhisperContext(model_path, dtype=dtype, gpu_device=local_rank, load_weights=(rank == 0 or world == 1))
     load_s = time.time() - t_load

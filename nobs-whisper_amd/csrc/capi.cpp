@@ -29,6 +29,9 @@ static whisper_context* make_ctx(const char* path, whisper_context_params cp, in
     }
     const int dev = cp.gpu_device >= 0 && cp.gpu_device < n_dev ? cp.gpu_device : 0;
     whisper_context* w = new whisper_context();
+    // dtype 2 = bf16 with the fp8 encoder GEMMs (large-v3-turbo fp8 config)
+    w->c.fp8_enc = dtype == 2;
+    if (dtype == 2) dtype = (int)DType::BF16;
     if (!load_context(&w->c, path, dev, (DType)dtype, load)) {
         free_context(&w->c);
         delete w;

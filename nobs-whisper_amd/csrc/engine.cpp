@@ -131,7 +131,7 @@ static void free_ws(Workspace& w) {
     // are freed with their parent
     void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
                   w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk,
-                  w.enc, w.qx, w.xo, w.xml, w.kvslot};
+                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs};
     for (void* p : ps) dfree(p);
     if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
     if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
@@ -175,7 +175,8 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
     size_t unused = 0;
     if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
-        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job}) dfree(p);
+        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job, (void*)w.hs}) dfree(p);
+        w.hs = nullptr;
         WM_CHECK(hipMalloc(&w.mel_img, (size_t)n_enc * 3002 * nm * E));
         WM_CHECK(hipMalloc(&w.h1, (size_t)n_enc * 3002 * d * E));
         WM_CHECK(hipMemset(w.h1, 0, (size_t)n_enc * 3002 * d * E));  // conv padding rows stay zero
@@ -184,6 +185,7 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         WM_CHECK(hipMalloc(&w.att, (size_t)n_enc * T * d * E));
         WM_CHECK(hipMalloc(&w.ff, (size_t)n_enc * T * 4 * d * E));
         WM_CHECK(hipMalloc((void**)&w.x, (size_t)n_enc * T * d * 4));
+        if (c->fp8_enc) WM_CHECK(hipMalloc((void**)&w.hs, (size_t)n_enc * T * sizeof(float)));
         WM_CHECK(hipMalloc((void**)&w.win_job, (size_t)n_enc * 3 * sizeof(int)));
         w.win_seek = w.win_job + n_enc;
         w.win_slot = w.win_job + 2 * n_enc;
@@ -325,6 +327,40 @@ static GemmArgs gemm_plain(const void* A, int M, int K, const void* B, int N, co
     return g;
 }
 
+// fp8 encoder weights: e4m3 copies of QKV, FC1 and FC2 with per-output-row scales, quantized on the
+// device from the bf16 weights once per context (after load or the RCCL weight broadcast).
+static void ensure_fp8(Context* c) {
+    std::lock_guard<std::mutex> lk(c->fp8_mu);
+    if (c->fp8_ready) return;
+    const Hparams& hp = c->hp;
+    const size_t d = hp.n_audio_state, nl = hp.n_audio_layer;
+    const size_t per = 3 * d * d + 4 * d * d + 4 * d * d, per_s = (3 * d + 4 * d + d) * sizeof(float);
+    WM_CHECK(hipSetDevice(c->device));
+    WM_CHECK(hipMalloc((void**)&c->arena8, nl * (per + per_s)));
+    c->enc8.assign(nl, Context::Fp8Layer{});
+    char* p = c->arena8;
+    for (size_t l = 0; l < nl; l++) {
+        Context::Fp8Layer& f = c->enc8[l];
+        const LayerW& L = c->w.enc[l];
+        f.wqkv = p; p += 3 * d * d;
+        f.w1 = p; p += 4 * d * d;
+        f.w2 = p; p += 4 * d * d;
+        f.sqkv = (float*)p; p += 3 * d * sizeof(float);
+        f.s1 = (float*)p; p += 4 * d * sizeof(float);
+        f.s2 = (float*)p; p += d * sizeof(float);
+        launch_quant_rows_fp8(c->dt, L.wqkv, 3 * d, (int)d, f.wqkv, f.sqkv, nullptr);
+        launch_quant_rows_fp8(c->dt, L.w1, 4 * d, (int)d, f.w1, f.s1, nullptr);
+        launch_quant_rows_fp8(c->dt, L.w2, d, (int)(4 * d), f.w2, f.s2, nullptr);
+    }
+    WM_CHECK(hipDeviceSynchronize());
+    c->fp8_ready = true;
+}
+
+static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float* sa, const float* sb, hipStream_t st) {
+    KT kt(s, K_GEMM_ENC, 2.0 * g.M * g.N * g.K, st);
+    launch_gemm_fp8(s->ctx->dt, epi, g, sa, sb, st);
+}
+
 int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* seeks, const int* slots, int n_win) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
@@ -334,6 +370,8 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
     const int KCLS = K_GEMM_ENC;
     const Weights& W = c->w;
     hipStream_t st = s->stream;
+    const bool fp8 = c->fp8_enc && d % 128 == 0;
+    if (fp8) ensure_fp8(c);
     for (int b0 = 0; b0 < n_win; b0 += w.cap_enc) {
         const int nb = std::min(w.cap_enc, n_win - b0);
         int* hi = w.h_ints;
@@ -360,6 +398,23 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
         const int M = nb * T;
         for (int l = 0; l < hp.n_audio_layer; l++) {
             const LayerW& L = W.enc[l];
+            if (fp8) {
+                // e4m3 path: LN quantized per row into hn (bytes), QKV/FC1/FC2 on the fp8 MFMA; the
+                // GELU output is re-quantized per row into the qkv buffer (free again after attention)
+                const Context::Fp8Layer& F = c->enc8[l];
+                launch_layernorm_fp8(w.x, M, d, L.ln1_w, L.ln1_b, w.hn, w.hs, st);
+                tgemm_fp8(s, EPI_STORE, gemm_plain(w.hn, M, d, F.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), w.hs, F.sqkv, st);
+                {
+                    KT kt(s, K_ATTN_ENC, 4.0 * nb * H * (double)T * T * 64);
+                    launch_attn_encoder(dt, w.qkv, w.att, nb, T, d, H, st);
+                }
+                tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
+                launch_layernorm_fp8(w.x, M, d, L.ln2_w, L.ln2_b, w.hn, w.hs, st);
+                tgemm_fp8(s, EPI_GELU, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
+                launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
+                tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
+                continue;
+            }
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln1_w, L.ln1_b, w.hn, st);
             tgemm(s, KCLS, dt, EPI_STORE, gemm_plain(w.hn, M, d, L.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), st);
             {

@@ -81,6 +81,15 @@ struct Context {
     bool cross_direct = false;
     std::string model_type;
     whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
+    // fp8 encoder (large-v3-turbo fp8 config): QKV, FC1 and FC2 as e4m3 GEMMs with per-row scales.
+    // The e4m3 weights are quantized from the loaded (or broadcast) bf16 weights on first use.
+    struct Fp8Layer { void* wqkv = nullptr; float* sqkv = nullptr; void* w1 = nullptr; float* s1 = nullptr;
+                      void* w2 = nullptr; float* s2 = nullptr; };
+    bool fp8_enc = false;
+    bool fp8_ready = false;
+    std::mutex fp8_mu;
+    std::vector<Fp8Layer> enc8;
+    char* arena8 = nullptr;
 };
 
 struct TokenData {
@@ -102,6 +111,7 @@ struct Workspace {
     // encoder (cap_enc windows)
     void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
     float* x = nullptr;
+    float* hs = nullptr;  // fp8 encoder: per-row scales of the quantized GEMM inputs
     // caches (cap_jobs slots). In direct mode `cross` is allocated on first use (prompts too long
     // for the direct prefill) and cross_fresh[slot] says whether a slot's cross K/V match enc.
     void *cross = nullptr, *self = nullptr;

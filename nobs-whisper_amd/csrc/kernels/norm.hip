@@ -54,6 +54,75 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     }
 }
 
+// LayerNorm with the output quantized to fp8 e4m3 (OCP) per row for the fp8 encoder GEMMs:
+// t = LN(x) * w + b in f32 (as layernorm_kernel, without the rounding to the MFMA type), then
+// s[i] = max|t| / 448, q[i][k] = e4m3(t[k] / s[i]). One wave per row.
+template <int NPL>
+__global__ void __launch_bounds__(256) layernorm_fp8_kernel(const float* __restrict__ x, int M, int D,
+                                                            const float* __restrict__ w, const float* __restrict__ b,
+                                                            uint8_t* __restrict__ q, float* __restrict__ s) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= M) return;
+    const float* xr = x + (long)i * D;
+    float v[NPL];
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        v[e] = k < D ? xr[k] : 0.0f;
+    }
+    double s1 = 0.0;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) s1 += (double)v[e];
+    for (int o = 32; o > 0; o >>= 1) s1 += __shfl_xor(s1, o);
+    const float mean = (float)(s1 / D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        v[e] = v[e] - mean;
+        if (k < D) s2 += (double)(v[e] * v[e]);
+    }
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    const float variance = (float)(s2 / D);
+    const float scale = 1.0f / sqrtf(variance + 1e-5f);
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        if (k < D) {
+            v[e] = (v[e] * scale) * w[k] + b[k];
+            amax = fmaxf(amax, fabsf(v[e]));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float sc = amax > 0.f ? amax / 448.f : 1.f, inv = 1.f / sc;
+    if (lane == 0) s[i] = sc;
+    uint8_t* qr = q + (long)i * D;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * e;
+        if (k < D) {
+            const float t = fminf(fmaxf(v[e] * inv, -448.f), 448.f);
+            qr[k] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(t, t, 0, false) & 0xff);
+        }
+    }
+}
+
+void launch_layernorm_fp8(const float* x, int M, int D, const float* w, const float* b, void* q, float* s,
+                          hipStream_t st) {
+    if (M <= 0) return;
+#define WM_LN8(N)                                                                                           \
+    if (D <= 64 * N) {                                                                                      \
+        layernorm_fp8_kernel<N><<<cdiv(M, 4), 256, 0, st>>>(x, M, D, w, b, (uint8_t*)q, s);                 \
+        return;                                                                                             \
+    }
+    WM_LN8(6) WM_LN8(8) WM_LN8(12) WM_LN8(16) WM_LN8(20) WM_LN8(24) WM_LN8(32)
+#undef WM_LN8
+    fprintf(stderr, "whisper_mi355x: layernorm width %d > 2048\n", D);
+    abort();
+}
+
 template <typename T>
 __global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__ pe, const int* __restrict__ tok,
                              const int* __restrict__ pos, int D, float* __restrict__ x) {

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libwhisper_mi355x.so")
 ENGINE_LIB_PATH = os.path.join(HERE, "lib", "libnobs_whisper_engine.so")
 
 F16, BF16 = 0, 1
+FP8_ENC = 2  # bf16 with the encoder QKV/FC1/FC2 GEMMs in fp8 e4m3 (large-v3-turbo fp8 config)
 GREEDY, BEAM_SEARCH = 0, 1
 
 
