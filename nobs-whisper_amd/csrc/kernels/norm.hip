@@ -109,9 +109,67 @@ __global__ void __launch_bounds__(256) layernorm_fp8_kernel(const float* __restr
     }
 }
 
+// the same with 4 consecutive columns per lane (D % 256 == 0): 16-byte row reads, 4-byte
+// coalesced fp8 stores (the strided form above stores single bytes)
+template <int NV>
+__global__ void __launch_bounds__(256) layernorm_fp8_v4_kernel(const float* __restrict__ x, int M, int D,
+                                                               const float* __restrict__ w, const float* __restrict__ b,
+                                                               uint8_t* __restrict__ q, float* __restrict__ s) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= M) return;
+    const float4* xr = (const float4*)(x + (long)i * D);
+    float4 v[NV];
+    double s1 = 0.0;
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+        v[e] = xr[lane + 64 * e];
+        s1 += (double)v[e].x + (double)v[e].y + (double)v[e].z + (double)v[e].w;
+    }
+    for (int o = 32; o > 0; o >>= 1) s1 += __shfl_xor(s1, o);
+    const float mean = (float)(s1 / D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+        v[e].x -= mean; v[e].y -= mean; v[e].z -= mean; v[e].w -= mean;
+        s2 += (double)(v[e].x * v[e].x) + (double)(v[e].y * v[e].y) + (double)(v[e].z * v[e].z) + (double)(v[e].w * v[e].w);
+    }
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+    const float scale = 1.0f / sqrtf((float)(s2 / D) + 1e-5f);
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+        const int k = 4 * (lane + 64 * e);
+        const float4 ww = *(const float4*)(w + k), bb = *(const float4*)(b + k);
+        v[e].x = (v[e].x * scale) * ww.x + bb.x; v[e].y = (v[e].y * scale) * ww.y + bb.y;
+        v[e].z = (v[e].z * scale) * ww.z + bb.z; v[e].w = (v[e].w * scale) * ww.w + bb.w;
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[e].x), fabsf(v[e].y)), fmaxf(fabsf(v[e].z), fabsf(v[e].w))));
+    }
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float sc = amax > 0.f ? amax / 448.f : 1.f, inv = 1.f / sc;
+    if (lane == 0) s[i] = sc;
+    uint32_t* qr = (uint32_t*)(q + (long)i * D);
+    auto c = [&](float t) { return fminf(fmaxf(t * inv, -448.f), 448.f); };
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+        uint32_t u = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[e].x), c(v[e].y), 0, false);
+        u = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[e].z), c(v[e].w), u, true);
+        qr[lane + 64 * e] = u;
+    }
+}
+
 void launch_layernorm_fp8(const float* x, int M, int D, const float* w, const float* b, void* q, float* s,
                           hipStream_t st) {
     if (M <= 0) return;
+    if (D % 256 == 0 && D <= 2048) {
+#define WM_LN8V(N)                                                                                          \
+        if (D == 256 * N) {                                                                                 \
+            layernorm_fp8_v4_kernel<N><<<cdiv(M, 4), 256, 0, st>>>(x, M, D, w, b, (uint8_t*)q, s);         \
+            return;                                                                                         \
+        }
+        WM_LN8V(2) WM_LN8V(3) WM_LN8V(4) WM_LN8V(5) WM_LN8V(6) WM_LN8V(8)
+#undef WM_LN8V
+    }
 #define WM_LN8(N)                                                                                           \
     if (D <= 64 * N) {                                                                                      \
         layernorm_fp8_kernel<N><<<cdiv(M, 4), 256, 0, st>>>(x, M, D, w, b, (uint8_t*)q, s);                 \

@@ -117,22 +117,26 @@ def test_gemm_fp8_matches_numpy(wrs, ctx, M, N, K, epi):
     assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
 
 
-def test_fp8_encoder_close_to_bf16(wrs, tiny_model):
-    """Whole encoder (tiny shape, 4 layers) with QKV/FC1/FC2 in e4m3 vs the same encoder in bf16:
+@pytest.mark.parametrize("shape,d", [("tiny", 384), ("base", 512)])
+def test_fp8_encoder_close_to_bf16(wrs, shape, d):
+    """Whole encoder (tiny: 4 layers, strided LN quantizer; base: 6 layers, the 16-byte one) with
+    QKV/FC1/FC2 in e4m3 vs the same encoder in bf16:
     not a parity path (e4m3 keeps 3 mantissa bits), so the bound is statistical: relative RMS error
     of the ln_post output < 0.1 and per-position cosine similarity > 0.99."""
+    from conftest import model_path
     from test_gpu_parity import gpu_mel
     sys_path_tools()
+    path = model_path(shape)
     from make_model import synthetic_pcm
     L = wrs.lib()
     pcm = synthetic_pcm(0)
     outs = []
     for dt in (wrs.BF16, wrs.FP8_ENC):
-        ctx = wrs.WhisperContext(tiny_model, dtype=dt)
+        ctx = wrs.WhisperContext(path, dtype=dt)
         st = ctx.create_state()
         gpu_mel(wrs, ctx, st, pcm)
         assert L.whisper_encode_with_state(ctx.ptr, st.ptr, 0, 1) == 0
-        out = np.empty((1500, 384), np.float32)
+        out = np.empty((1500, d), np.float32)
         assert L.whisper_mi355x_get_encoder_out(st.ptr, out.ctypes.data_as(C.POINTER(C.c_float)), out.size) == 0
         outs.append(out)
         st.close()
@@ -141,7 +145,7 @@ def test_fp8_encoder_close_to_bf16(wrs, tiny_model):
     assert np.isfinite(got).all()
     rel = np.sqrt(np.mean((got - ref) ** 2) / np.mean(ref ** 2))
     cos = (got * ref).sum(1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
-    print(f"fp8 encoder: relative RMS error {rel:.4f}, min cosine {cos.min():.5f}")
+    print(f"fp8 encoder ({shape}): relative RMS error {rel:.4f}, min cosine {cos.min():.5f}")
     assert rel < 0.1, rel
     assert cos.min() > 0.99, cos.min()
 
