@@ -15,8 +15,10 @@
 extern "C" {
 #endif
 
-/* compute type of weights and GEMM activations */
-enum whisper_mi355x_dtype { WHISPER_MI355X_F16 = 0, WHISPER_MI355X_BF16 = 1 };
+/* compute type of weights and GEMM activations. FP8_ENC: bf16, with the encoder's QKV, FC1 and FC2
+ * GEMMs on OCP e4m3 weights and activations (per-row f32 scales; the large-v3-turbo fp8 config).
+ * FP8_ENC is a throughput mode, not a whisper.cpp-parity mode. */
+enum whisper_mi355x_dtype { WHISPER_MI355X_F16 = 0, WHISPER_MI355X_BF16 = 1, WHISPER_MI355X_FP8_ENC = 2 };
 
 /* Context on HIP device `gpu_device` (from params) with an explicit compute type.
  * load_weights = false: parse the file and allocate the device weight arena without filling it
