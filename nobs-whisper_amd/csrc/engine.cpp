@@ -410,7 +410,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
                 }
                 tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
                 launch_layernorm_fp8(w.x, M, d, L.ln2_w, L.ln2_b, w.hn, w.hs, st);
-                tgemm_fp8(s, EPI_GELU, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
+                tgemm_fp8(s, EPI_GELU_F, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
                 launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
                 tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
                 continue;

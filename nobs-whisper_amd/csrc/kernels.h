@@ -32,6 +32,7 @@ enum Epi : int {
     EPI_F32 = 4,       // f32 out = v                                       (logits)
     EPI_CROSSKV = 5,   // T scatter into cross cache [slot][L][2][H][ctx][64]; K columns scaled
     EPI_QKV_DEC = 6,   // n<d: T q[m][n]*scale ; d<=n<2d: K cache (scaled) ; 2d<=n<3d: V cache
+    EPI_GELU_F = 7,    // T out = tanh-GELU by formula in f32 (fp8 mode only: not ggml's f16 table)
 };
 
 struct GemmArgs {

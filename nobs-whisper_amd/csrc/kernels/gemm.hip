@@ -83,6 +83,13 @@ __device__ __forceinline__ void gelu_ltab_stage(char* dst, int tid) {
     }
 }
 
+// tanh-GELU by formula, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)), for the fp8 mode (which is not
+// a whisper.cpp-parity path, so it skips the table and its 75.8 KB LDS copy per tile)
+__device__ __forceinline__ float gelu_formula(float x) {
+    const float u = 1.5957691216057308f * (x + 0.044715f * x * x * x);
+    return x / (1.0f + __expf(-u));
+}
+
 template <int EPI, typename T>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float v) {
     if (g.bias) v = v + g.bias[n];
@@ -93,6 +100,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
     } else if constexpr (EPI == EPI_GELU) {
         const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
         ((T*)g.out)[orow * g.ldo + n] = (T)gelu_tab(v);
+    } else if constexpr (EPI == EPI_GELU_F) {
+        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
+        ((T*)g.out)[orow * g.ldo + n] = (T)gelu_formula(v);
     } else if constexpr (EPI == EPI_RESID) {
         float* o = (float*)g.out + (long)m * g.ldo + n;
         *o = v + *o;
@@ -126,7 +136,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     bool vec = n + 16 <= g.N && EPI != EPI_QKV_DEC;
     long base = 0;
-    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_F) {
         const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
         base = orow * g.ldo + n;
         vec = vec && (((uintptr_t)((T*)g.out + base)) & 15) == 0;
@@ -147,7 +157,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
             v[k] = v[k] + b.x; v[k + 1] = v[k + 1] + b.y; v[k + 2] = v[k + 2] + b.z; v[k + 3] = v[k + 3] + b.w;
         }
     }
-    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_CROSSKV) {
+    if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_F || EPI == EPI_CROSSKV) {
         float sc = 1.0f;
         T* dst;
         if constexpr (EPI == EPI_CROSSKV) {
@@ -166,6 +176,7 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
         for (int k = 0; k < 16; k++) {
             float x = v[k];
             if constexpr (EPI == EPI_GELU) x = LTAB ? gelu_ltab(x, ltab) : gelu_tab(x);
+            else if constexpr (EPI == EPI_GELU_F) x = gelu_formula(x);
             else if (sc != 1.0f) x = x * sc;
             o[k] = (T)x;
         }
@@ -1303,6 +1314,7 @@ static void launch_mx_t(int epi, const GemmArgs& g, const float* sa, const float
     switch (epi) {
         case EPI_STORE: gemm8p_mx_kernel<T, EPI_STORE><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_GELU: gemm8p_mx_kernel<T, EPI_GELU><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        case EPI_GELU_F: gemm8p_mx_kernel<T, EPI_GELU_F><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_RESID: gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         default: fprintf(stderr, "whisper_mi355x: fp8 GEMM epilogue %d not supported\n", epi); abort();
     }

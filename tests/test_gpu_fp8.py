@@ -84,7 +84,7 @@ def test_quant_rows_fp8(wrs, ctx, rows, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 1280, 1280), (512, 3840, 1280), (257, 768, 3072), (1500, 1280, 5120)])
-@pytest.mark.parametrize("epi", [0, 2])
+@pytest.mark.parametrize("epi", [0, 2, 7])
 def test_gemm_fp8_matches_numpy(wrs, ctx, M, N, K, epi):
     L = wrs.lib()
     L.whisper_mi355x_debug_gemm_fp8.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
@@ -97,6 +97,8 @@ def test_gemm_fp8_matches_numpy(wrs, ctx, M, N, K, epi):
     sa = rng.uniform(0.001, 0.01, M).astype(np.float32)
     sb = rng.uniform(0.0001, 0.001, N).astype(np.float32)
     bias = rng.standard_normal(N).astype(np.float32)
+    if epi == 7:  # EPI_GELU_F: scale the pre-activations to O(1) so the GELU's bend is exercised
+        sb = sb * 0.1
     out0 = np.zeros((M, N), np.float32 if epi == 2 else np.float16)
     ptrs = [_dev(L, ctx, a) for a in (A8, sa, B8, sb, bias, out0)]
     pa, psa, pb, psb, pbias, po = ptrs
@@ -111,7 +113,10 @@ def test_gemm_fp8_matches_numpy(wrs, ctx, M, N, K, epi):
     ref = (a64 @ b64.T) * sa[:, None].astype(np.float64) * sb[None, :].astype(np.float64) + bias
     mag = (np.abs(a64) @ np.abs(b64).T) * sa[:, None] * sb[None, :]
     bound = 1e-4 * mag + 1e-6
-    if epi == 0:  # f16 output: + half an f16 ulp
+    if epi == 7:  # tanh-GELU (slope <= 1.13), __expf: + 1e-6 relative
+        ref = 0.5 * ref * (1.0 + np.tanh(np.sqrt(2.0 / np.pi) * (ref + 0.044715 * ref ** 3)))
+        bound = 1.13 * bound + 1e-6 * np.abs(ref)
+    if epi in (0, 7):  # f16 output: + half an f16 ulp
         bound = bound + np.abs(ref) * 2.0 ** -11 + 2.0 ** -24
     err = np.abs(out - ref)
     assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
