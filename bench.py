@@ -2,15 +2,19 @@
 """Throughput benchmark: audio-seconds/s of greedy Whisper transcription on MI355X.
 
 Metric (BASELINE.json): "audio-sec/s (RTF^-1) large-v3 greedy, batch 128; 1/2/4/8 MI355X".
-One step = whisper_mi355x_full_batch over this rank's batch of 30 s chunks (PCM already resident
-in HBM): log-mel -> encoder -> cross-KV -> prefill -> fixed-work greedy decode of --tokens tokens
-per chunk (EOT suppressed, no fallback: SURVEY.md §8d's reproducible-work mode for random
-weights) -> logits processing -> segments. Weak scaling: every rank processes --batch chunks;
-ranks shard chunks with no data-path collective; weights are loaded by rank 0 and broadcast once
-over RCCL/xGMI (outside the timed region).
+One step = whisper_mi355x_full_batch over this rank's share of a global batch of 30 s chunks (PCM
+already resident in HBM): log-mel -> encoder -> cross attention -> prefill -> fixed-work greedy
+decode of --tokens tokens per chunk (EOT suppressed, no fallback: SURVEY.md §8d's reproducible-work
+mode for random weights) -> logits processing -> segments.
 
-Model weights are a seeded synthetic GGML file of the named architecture (no checkpoints
-offline); audio is synthetic (tools/make_model.synthetic_pcm, seed 1234+chunk index).
+Multi-GPU (BASELINE config 4): strong scaling of --global-batch chunks (default 128):
+rank r transcribes chunks [r*ceil(B/n), min(B, (r+1)*ceil(B/n))); ranks share no data-path
+collective; rank 0 loads the weights and broadcasts the packed arena once over RCCL/xGMI (outside
+the timed region, reported as weight_broadcast_s). `--gpus N` without a torch.distributed launcher
+spawns the N rank processes itself (before any GPU call); under torchrun it reads RANK/WORLD_SIZE.
+
+Model weights are a seeded synthetic GGML file of the named architecture (no checkpoints offline);
+audio is synthetic (tools/make_model.synthetic_pcm, seed 1234 + global chunk index).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -35,6 +39,9 @@ K_BOUND = ["mfma", "mfma", "hbm", "hbm", "hbm", "hbm", "hbm"]
 SINGLE_KERNEL = [1, 2, 3, 5, 6]  # classes that are one kernel each (attention, logits, mel)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0       # dense bf16/f16 MFMA peak (no sparsity)
+FP8_PEAK_TFS = 5000.0        # dense fp8 MFMA peak
+# PMC traffic pass of the roofline kernel (tools/pmc.sh -> tools/pmc_traffic.py), chosen by name
+PMC_TRAFFIC_FILE = "r01f_pmc_traffic.json"
 
 
 def log(*a):
@@ -56,6 +63,21 @@ def ensure_model(path: str, shape: str):
         t = time.time()
         write_model(path, shape, 0)
         log(f"[bench] wrote synthetic {shape} model to {path} in {time.time() - t:.1f}s")
+
+
+def host_cpu() -> dict:
+    """The node's CPU as the driver box reports it (lscpu model name, logical CPUs) and the share
+    this job may use (OMP_NUM_THREADS on the box; the cgroup gives one GPU's job 16 CPUs)."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    share = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    return dict(model=model, logical_cpus=os.cpu_count(), affinity=len(os.sched_getaffinity(0)), share=share)
 
 
 def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: int = 8) -> dict:
@@ -84,11 +106,14 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
     o.close()
     per_step = (t4 - t3) / n_sample_tokens
     chunk_s = (t1 - t0) + (t2 - t1) + (t3 - t2) + n_tokens * per_step
-    return dict(value=30.0 / chunk_s, unit="audio-sec/s", cores=threads, kind="port",
+    cpu = host_cpu()
+    return dict(value=round(30.0 / chunk_s, 3), unit="audio-sec/s", cores=threads, kind="port",
+                host_cpu=cpu,
                 sample=(f"1 x 30 s chunk: mel {t1 - t0:.2f}s + encoder/cross-KV {t2 - t1:.2f}s + prefill {t3 - t2:.2f}s "
                         f"+ {n_sample_tokens} decode steps ({per_step * 1e3:.0f} ms/step) measured, extrapolated to "
                         f"{n_tokens} steps/chunk; oracle/ = restated whisper.cpp CPU algorithm (not whisper.cpp), "
-                        f"{threads} OpenMP threads"))
+                        f"{threads} OpenMP threads = this job's CPU share of a {cpu['logical_cpus']}-CPU "
+                        f"{cpu['model']} host"))
 
 
 # kernel symbols of each class in the rocprofv3 PMC output (tools/pmc.sh -> tools/pmc_traffic.py)
@@ -98,15 +123,14 @@ K_SYMBOL = {"gemm_encoder": r"gemm256_kernel", "attn_encoder": r"attn_enc2_kerne
 
 def pmc_traffic(kernel_class: str, grid_threads: int | None = None):
     """Launch-weighted HBM bytes per launch of the class's kernel (restricted to launches of
-    `grid_threads` threads when given) from the newest committed profiles/*_pmc_traffic.json
-    (FETCH_SIZE doubled per the gfx950 correction, + WRITE_SIZE), or None when no PMC pass covers it."""
-    import glob
+    `grid_threads` threads when given) from profiles/PMC_TRAFFIC_FILE (FETCH_SIZE doubled per the
+    gfx950 correction, + WRITE_SIZE), or None when that pass does not cover it."""
     import re
     pat = K_SYMBOL.get(kernel_class)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
-    if not pat or not files:
+    path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
+    if not pat or not os.path.exists(path):
         return None, None
-    with open(files[-1]) as f:
+    with open(path) as f:
         data = json.load(f)
     n = tb = 0.0
     for sym, v in data.items():
@@ -114,13 +138,14 @@ def pmc_traffic(kernel_class: str, grid_threads: int | None = None):
         if re.search(pat, name) and (grid_threads is None or grid == str(grid_threads)):
             n += v["launches"]
             tb += v["traffic_bytes"] * v["launches"]
-    return (tb / n if n else None), os.path.basename(files[-1])
+    return (tb / n if n else None), PMC_TRAFFIC_FILE
 
 
-def rank_chunk_ids(rank: int, batch: int) -> list[int]:
-    """Weak-scaling shard: rank r transcribes chunks r*batch ... r*batch+batch-1 (independent
-    30 s chunks; no data-path exchange between ranks)."""
-    return [rank * batch + i for i in range(batch)]
+def rank_chunk_ids(rank: int, world: int, global_batch: int) -> list[int]:
+    """Strong-scaling shard: contiguous blocks of ceil(B/n) chunks per rank; the last
+    rank may get fewer. Independent 30 s chunks: no data-path exchange between ranks."""
+    per = -(-global_batch // world)
+    return list(range(rank * per, min(global_batch, (rank + 1) * per)))
 
 
 def max_over_ranks(x: float, dist, device: str) -> float:
@@ -133,24 +158,91 @@ def max_over_ranks(x: float, dist, device: str) -> float:
     return float(t.item())
 
 
+def phase_work(shape: str, n_chunks: int, tokens: int, prompt_len: int, direct: bool) -> dict:
+    """Algorithmic work of one step: encoder FLOPs (conv stem + layers incl.
+    attention) and the decode steps' HBM bytes (decoder weights + token embedding once per step,
+    the encoder output E once per clip and layer (direct cross attention; the K + V cache when not
+    direct), the self-KV prefix)."""
+    from make_model import SHAPES as S
+    V, nm, d, h, Le, Ld = S[shape]
+    T = 1500
+    conv = 2.0 * 2 * T * 3 * nm * d + 2.0 * T * 3 * d * d
+    layer = 2.0 * T * d * 12 * d + 4.0 * T * T * d
+    enc_flops = n_chunks * (conv + Le * layer)
+    w_bytes = (Ld * 16 * d * d + V * d) * 2.0
+    xa_bytes = n_chunks * Ld * T * d * 2.0 * (1 if direct else 2)
+    avg_pos = prompt_len + tokens / 2.0
+    self_bytes = n_chunks * Ld * 2 * avg_pos * d * 2.0
+    return dict(enc_flops=enc_flops, dec_bytes_per_step=w_bytes + xa_bytes + self_bytes,
+                dec_weight_bytes=w_bytes, dec_cross_bytes=xa_bytes, dec_self_bytes=self_bytes)
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes (one per GPU) with the torch.distributed
+    env, before this process touches the GPU; return the worst exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def plan(rank: int, world: int, args) -> None:
+    """--plan: the multi-rank layout without a GPU (tests/test_dist.py): every rank joins a gloo
+    group, computes its shard and a rank-dependent "elapsed", and rank 0 prints the max over ranks
+    and the gathered shard map as one JSON line."""
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    ids = rank_chunk_ids(rank, world, args.global_batch)
+    t = max_over_ranks(0.25 * (rank + 1), dist, "cpu")
+    shards = [ids]
+    if dist is not None:
+        shards = [None] * world
+        dist.all_gather_object(shards, ids)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"world": world, "max_elapsed": t, "shards": shards}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="large-v3")
-    ap.add_argument("--batch", type=int, default=128, help="30 s chunks per GPU")
+    ap.add_argument("--global-batch", type=int, default=128, help="30 s chunks per step over all GPUs (strong scaling)")
+    ap.add_argument("--batch", type=int, default=0, help="weak scaling instead: chunks per GPU (0 = off)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"],
                     help="fp8: bf16 with the encoder QKV/FC1/FC2 GEMMs on e4m3 weights + activations")
     ap.add_argument("--tokens", type=int, default=128, help="decode tokens per chunk (fixed-work mode)")
+    ap.add_argument("--variants", type=int, default=1,
+                    help="also time the reference's prompted (default vocabulary) and auto-language workloads")
+    ap.add_argument("--variant-steps", type=int, default=3)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this job's CPU share (OMP_NUM_THREADS)")
     ap.add_argument("--model-dir", default=os.environ.get("NW_MODEL_DIR", "/tmp/nw_models"))
+    ap.add_argument("--plan", action="store_true",
+                    help="CPU dry run of the rank layout: gloo group, shard map and max-over-ranks, no GPU")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plan:
+        return plan(rank, world, args)
     import numpy as np
     import torch
     dist = None
@@ -182,34 +274,53 @@ def main():
             assert wrs.lib().whisper_mi355x_rccl_unique_id(uid) == 0
         obj = [bytes(uid.raw)]
         dist.broadcast_object_list(obj, src=0)
+        barrier()
         t = time.time()
         rc = wrs.lib().whisper_mi355x_broadcast_weights(ctx.ptr, obj[0], rank, world)
         assert rc == 0, rc
-        bcast_s = time.time() - t
+        bcast_s = max_over_ranks(time.time() - t, dist, "cuda")
     st = ctx.create_state()
 
     # ---- this rank's chunks, resident in HBM --------------------------------------------------------
     from make_model import synthetic_pcm
     L = wrs.lib()
     n = 16000 * 30
-    buf = L.whisper_mi355x_dev_alloc(ctx.ptr, args.batch * n * 4)
+    if args.batch > 0:
+        ids = [rank * args.batch + i for i in range(args.batch)]
+        global_batch = args.batch * world
+    else:
+        ids = rank_chunk_ids(rank, world, args.global_batch)
+        global_batch = args.global_batch
+    nb = len(ids)
+    buf = L.whisper_mi355x_dev_alloc(ctx.ptr, max(1, nb) * n * 4)
     assert buf
     host = np.empty(n, np.float32)
-    for i, cid in enumerate(rank_chunk_ids(rank, args.batch)):
+    for i, cid in enumerate(ids):
         host[:] = synthetic_pcm(cid)
         L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(buf + i * n * 4), host.ctypes.data, n * 4, 1)
-    jobs = [(buf + i * n * 4, n) for i in range(args.batch)]
+    jobs = [(buf + i * n * 4, n) for i in range(nb)]
+
+    def step(params):
+        if nb:
+            rc = st.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
+            assert rc == 0, rc
+
+    def timed(params, steps):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(steps):
+            step(params)
+        torch.cuda.synchronize()
+        barrier()
+        return max_over_ranks(time.time() - t0, dist, "cuda")
+
     params = wrs.reference_full_params("en")
-
-    def step():
-        rc = st.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
-        assert rc == 0, rc
-
     # warmup (untimed) with every kernel class timed once to find the dominant kernel
     L.whisper_mi355x_kernel_timing(st.ptr, 0x7F)
     tw = time.time()
     for _ in range(args.warmup):
-        step()
+        step(params)
     warm_s = (time.time() - tw) / max(1, args.warmup)
     stats = []
     for k in range(len(K_NAMES)):
@@ -219,28 +330,38 @@ def main():
     # the roofline kernel: the largest single kernel. The two GEMM classes hold many kernels (every
     # projection shape and epilogue), so they are excluded; timing one of them would also put an
     # event pair around ~8 launches per layer inside the decode graphs and slow the timed region.
+    # Their phases are reported below (roofline.phases) from the phase clocks.
     dom = max(SINGLE_KERNEL, key=lambda k: stats[k][0])
     share = {K_NAMES[k]: round(stats[k][0] / max(1e-9, sum(s[0] for s in stats)), 4) for k in range(len(K_NAMES))}
 
     # timed region: only the dominant class is event-timed (keeps event overhead off the others)
     L.whisper_mi355x_kernel_timing(st.ptr, 1 << dom)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.time()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.time() - t0
-    elapsed = max_over_ranks(elapsed, dist, "cuda")
+    elapsed = timed(params, args.steps)
     out = (C.c_double * 3)()
     L.whisper_mi355x_kernel_stats(st.ptr, dom, out)
     k_ms, k_cnt, k_work = out[0], out[1], out[2]
     phases = st.phase_ms()
     decoded = L.whisper_mi355x_batch_decoded_tokens(st.ptr)
+    L.whisper_mi355x_kernel_timing(st.ptr, 0)
+
+    # the reference's own workloads: the app always passes its default vocabulary as
+    # the initial prompt (config.rs:40-42, whisper.rs:98-109) with language "auto" (config.rs:49)
+    variants = []
+    if args.variants:
+        for name, p in (("prompted (default vocabulary, config.rs:40-42), language en",
+                         wrs.reference_full_params("en", initial_prompt=wrs.DEFAULT_VOCABULARY)),
+                        ("auto language (config.rs:49), no prompt", wrs.reference_full_params(None)),
+                        ("reference default: auto language + default vocabulary prompt",
+                         wrs.reference_full_params(None, initial_prompt=wrs.DEFAULT_VOCABULARY))):
+            step(p)  # warmup (builds the graphs / cross caches of this shape)
+            el = timed(p, args.variant_steps)
+            variants.append(dict(workload=name, value=round(30.0 * global_batch * args.variant_steps / el, 2),
+                                 ms_per_step=round(1e3 * el / args.variant_steps, 2),
+                                 prompt_tokens=len(ctx.tokenize(wrs.DEFAULT_VOCABULARY)) if "vocabulary" in name else 0,
+                                 phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
 
     if rank == 0:
-        audio_s = 30.0 * args.batch * world * args.steps
+        audio_s = 30.0 * global_batch * args.steps
         value = audio_s / elapsed
         if K_BOUND[dom] == "mfma":
             achieved = k_work / (k_ms * 1e-3) / 1e12
@@ -252,31 +373,54 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
         grid = None
         if K_NAMES[dom] == "attn_cross_decode":  # decode-step launches: splits x clips workgroups of 512
-            grid = max(1, min(16, -(-256 // args.batch))) * args.batch * 512
+            grid = max(1, min(16, -(-256 // nb))) * nb * 512
         traffic, src = pmc_traffic(K_NAMES[dom], grid)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                         traffic_source=f"profiles/{src}")
         roof.update(kernel=K_NAMES[dom], launches=int(k_cnt), avg_launch_ms=round(k_ms / max(1, k_cnt), 4),
                     work_per_launch=k_work / max(1, k_cnt), time_share_warmup=share)
+        # per-phase, time-weighted rooflines of rank 0's last step (phase clocks are host wall time
+        # around stream-synchronised phases)
+        pw = phase_work(args.model, nb, args.tokens, 3, True)
+        enc_s = phases["encode"] * 1e-3
+        dec_s = phases["decode"] * 1e-3
+        mfma_peak = FP8_PEAK_TFS if args.dtype == "fp8" else MFMA_PEAK_TFS
+        roof["phases"] = {
+            "encode": dict(bound="mfma", ms=round(phases["encode"], 1), tflop=round(pw["enc_flops"] / 1e12, 2),
+                           achieved=round(pw["enc_flops"] / max(1e-9, enc_s) / 1e12, 1), unit="TFLOP/s",
+                           peak=MFMA_PEAK_TFS, frac=round(pw["enc_flops"] / max(1e-9, enc_s) / 1e12 / MFMA_PEAK_TFS, 4),
+                           note=("bf16 peak; fp8 mode runs QKV/FC1/FC2 on the fp8 pipe (peak %.0f)" % mfma_peak)
+                           if args.dtype == "fp8" else None),
+            "decode": dict(bound="hbm", ms=round(phases["decode"], 1), steps=args.tokens - 1,
+                           gb_per_step=round(pw["dec_bytes_per_step"] / 1e9, 3),
+                           achieved=round(pw["dec_bytes_per_step"] * (args.tokens - 1) / max(1e-9, dec_s) / 1e9, 1),
+                           unit="GB/s", peak=HBM_PEAK_GBS,
+                           frac=round(pw["dec_bytes_per_step"] * (args.tokens - 1) / max(1e-9, dec_s) / 1e9 / HBM_PEAK_GBS, 4),
+                           bytes_split_gb={k: round(pw[k] / 1e9, 3) for k in ("dec_weight_bytes", "dec_cross_bytes", "dec_self_bytes")}),
+        }
         cpu = None
         if args.cpu_baseline and world == 1:
+            threads = args.cpu_threads or host_cpu()["share"]
             try:
-                cpu = cpu_baseline(model_path, args.cpu_threads, args.tokens)
+                cpu = cpu_baseline(model_path, threads, args.tokens)
             except Exception as e:  # reported, never fatal to the GPU number
-                cpu = dict(value=None, unit="audio-sec/s", cores=args.cpu_threads, kind="port", sample=f"failed: {e}")
+                cpu = dict(value=None, unit="audio-sec/s", cores=threads, kind="port", sample=f"failed: {e}")
+        scaling = "weak" if args.batch > 0 else "strong"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "audio-sec/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "scaling": scaling, "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded AM-harmonic 30 s PCM; seeded random weights of the named architecture)",
-            "config": {"workload": f"{args.model} {args.dtype} greedy, {args.batch} x 30 s chunks per GPU, "
-                                   f"fixed {args.tokens}-token decode per chunk, language en, no prompt",
-                       "model": args.model, "global_batch": args.batch * world, "batch_per_gpu": args.batch,
+            "config": {"workload": f"{args.model} {args.dtype} greedy, {global_batch} x 30 s chunks per step over "
+                                   f"{world} GPU(s) ({nb} on rank 0), fixed {args.tokens}-token decode per chunk, "
+                                   f"language en, no prompt",
+                       "model": args.model, "global_batch": global_batch, "batch_per_gpu": nb,
                        "tokens_per_chunk": args.tokens, "seq_len": 1500,
                        "parallelism": f"dp{world} (chunk sharding, RCCL weight broadcast only)"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "variants": variants,
             "extra": {"rtf_inverse_per_gpu": round(value / world, 2), "decoded_tokens_per_step": decoded,
                       "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
                       "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),

@@ -52,6 +52,29 @@ WHISPER_API int whisper_mi355x_batch_lang_id(struct whisper_state * state, int j
 /* tokens generated (all decode steps, all attempts) by the last whisper_mi355x_full_batch */
 WHISPER_API long whisper_mi355x_batch_decoded_tokens(struct whisper_state * state);
 
+/* Per-window decisions of whisper_full's temperature-fallback loop (the integer outcomes that are
+ * comparable with whisper.cpp even when a sampled t > 0 attempt is not): one record per decoded
+ * 30 s window, in seek order. temp_idx: index of the temperature finally used (0 = greedy t = 0
+ * succeeded); n_attempts = temp_idx + 1; failed0: the t = 0 attempt failed (timestamp rule or
+ * entropy < entropy_thold); logprob_fail0: its avg_logprob < logprob_thold; result_len0,
+ * avg_logprob0, entropy0: that attempt's sequence score inputs; no_speech: the window was
+ * dropped as silence. job = 0 for whisper_full_with_state. Returns the record count (or -count
+ * when cap is too small). */
+struct whisper_mi355x_window_decision {
+    int32_t seek;
+    int32_t temp_idx;
+    int32_t failed0;
+    int32_t logprob_fail0;
+    int32_t result_len0;
+    int32_t no_speech;
+    float   avg_logprob0;
+    float   entropy0;
+    float   no_speech_prob;
+    float   pad;
+};
+WHISPER_API int whisper_mi355x_window_decisions(struct whisper_state * state, int job,
+                                                struct whisper_mi355x_window_decision * out, int cap);
+
 /* Phase timings of the last full/full_batch call, milliseconds (host wall clock around
  * stream-synchronised phases): mel, encode (incl. cross-KV), prefill, decode steps, logits. */
 WHISPER_API int whisper_mi355x_phase_ms(struct whisper_state * state, double out[5]);

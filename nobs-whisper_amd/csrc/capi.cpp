@@ -158,7 +158,8 @@ void whisper_free_state(struct whisper_state* s) { free_state(s); }
 void whisper_free(struct whisper_context* ctx) {
     if (!ctx) return;
     if (ctx->c.default_state) free_state(ctx->c.default_state);
-    if (ctx->c.arena) { hipSetDevice(ctx->c.device); hipFree(ctx->c.arena); }
+    ctx->c.default_state = nullptr;
+    free_context(&ctx->c);  // weight arena + the fp8 arena
     delete ctx;
 }
 
@@ -422,6 +423,13 @@ int whisper_mi355x_batch_lang_id(struct whisper_state* s, int job) {
     return s && job >= 0 && job < (int)s->lang_ids.size() ? s->lang_ids[job] : -1;
 }
 long whisper_mi355x_batch_decoded_tokens(struct whisper_state* s) { return s ? s->decoded_tokens : 0; }
+int whisper_mi355x_window_decisions(struct whisper_state* s, int job, struct whisper_mi355x_window_decision* out, int cap) {
+    if (!s || job < 0 || job >= (int)s->decisions.size()) return 0;
+    const auto& d = s->decisions[job];
+    if ((int)d.size() > cap) return -(int)d.size();
+    for (size_t i = 0; i < d.size(); i++) out[i] = d[i];
+    return (int)d.size();
+}
 int whisper_mi355x_phase_ms(struct whisper_state* s, double out[5]) {
     if (!s) return -1;
     for (int i = 0; i < 5; i++) out[i] = s->phase_ms[i];

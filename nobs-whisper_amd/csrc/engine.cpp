@@ -703,6 +703,8 @@ struct Job {
     Phase phase = PH_ENCODE;
     std::vector<Segment> result;
     int n_new_segments = 0;
+    whisper_mi355x_window_decision dec{};                // the current window's fallback decisions
+    std::vector<whisper_mi355x_window_decision> decisions;
 };
 
 struct Sched {
@@ -818,6 +820,11 @@ static void finish_window(Sched& S, Job& j) {
         }
     }
     j.n_new_segments = (int)(j.result.size() - n_before);
+    j.dec.seek = j.seek;
+    j.dec.temp_idx = j.temp_idx;
+    j.dec.no_speech = is_no_speech;
+    j.dec.no_speech_prob = j.no_speech_prob;
+    j.decisions.push_back(j.dec);
     j.seek += seek_delta;
     j.phase = (j.seek + 10 >= j.seek_end) ? PH_DONE : PH_ENCODE;
 }
@@ -827,6 +834,14 @@ static void attempt_done(Sched& S, Job& j) {
         j.tokens.resize(j.result_len);
         score_seq(S.p, j);
         if (j.result_len > 32 && j.entropy < S.p.entropy_thold) j.failed = true;
+    }
+    if (j.temp_idx == 0) {  // the greedy attempt's outcome (comparable with whisper.cpp bit for bit)
+        j.dec = whisper_mi355x_window_decision{};
+        j.dec.failed0 = j.failed;
+        j.dec.logprob_fail0 = j.avg_logprobs < S.p.logprob_thold;
+        j.dec.result_len0 = j.result_len;
+        j.dec.avg_logprob0 = (float)j.avg_logprobs;
+        j.dec.entropy0 = (float)j.entropy;
     }
     bool success = true;
     if (j.temp_idx != (int)S.temps.size() - 1)
@@ -983,9 +998,16 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
 int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                int n_jobs, bool on_device, const FullOpts& o, bool single_api) {
     WM_CHECK(hipSetDevice(c->device));
-    if (p.strategy != WHISPER_SAMPLING_GREEDY || p.greedy.best_of > 1) {
-        fprintf(stderr, "whisper_mi355x: only greedy best_of=1 (the reference's strategy, whisper.rs:88) is implemented\n");
+    if (p.strategy != WHISPER_SAMPLING_GREEDY) {
+        fprintf(stderr, "whisper_mi355x: beam search is not implemented (the reference uses Greedy, whisper.rs:88)\n");
         return -100;
+    }
+    if (p.greedy.best_of > 1) {
+        // whisper.cpp uses best_of only for sampled (t > 0) fallback attempts: t = 0 is unaffected.
+        // Sampled attempts here run one candidate per clip (the reference's Greedy{best_of: 1}).
+        static bool warned = false;
+        if (!warned) fprintf(stderr, "whisper_mi355x: greedy best_of=%d: fallback attempts sample 1 candidate\n", p.greedy.best_of);
+        warned = true;
     }
     Sched S;
     S.c = c; S.s = s; S.p = p; S.o = o; S.single_api = single_api;
@@ -993,6 +1015,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
     const Hparams& hp = c->hp;
     s->results.assign(n_jobs, {});
     s->lang_ids.assign(n_jobs, 0);
+    s->decisions.assign(n_jobs, {});
     s->decoded_tokens = 0;
     double t0 = now_ms();
     ensure_ws(c, s, n_jobs);
@@ -1001,7 +1024,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
 
     if (p.temperature_inc > 0.0f && o.fixed_tokens <= 0)
         for (float t = p.temperature; t < 1.0f + 1e-6f; t += p.temperature_inc) S.temps.push_back(t);
-    else S.temps.push_back(p.temperature);
+    if (S.temps.empty()) S.temps.push_back(p.temperature);
     const int n_max = hp.n_text_ctx / 2 - 4;
     S.n_max_steps = o.fixed_tokens > 0 ? o.fixed_tokens : n_max;
     const bool need_lang = p.language == nullptr || strlen(p.language) == 0 || strcmp(p.language, "auto") == 0 || p.detect_language;
@@ -1029,7 +1052,11 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
             for (int t : init_prompt_tokens) j.prompt_past.push_back(t);
             std::rotate(j.prompt_past.begin(), j.prompt_past.end() - init_prompt_tokens.size(), j.prompt_past.end());
         }
-        if (need_lang && 0 >= j.n_len_org) { j.phase = PH_DONE; continue; }  // whisper: lang detect fails -> -3
+        if (need_lang && 0 >= j.n_len_org) {  // whisper_full_with_state: failed auto-detect -> -3
+            if (single_api) return -3;
+            j.phase = PH_DONE;
+            continue;
+        }
         if (j.seek_end < j.seek_start + 10) { j.phase = PH_DONE; continue; }
         j.lang_pending = need_lang;
         if (!need_lang) j.lang_id = lang_index(p.language);
@@ -1196,6 +1223,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
     for (int k = 0; k < n_jobs; k++) {
         s->results[k] = std::move(S.jobs[k].result);
         s->lang_ids[k] = S.jobs[k].lang_id;
+        s->decisions[k] = std::move(S.jobs[k].decisions);
     }
     if (single_api && n_jobs > 0) {
         s->prompt_past = S.jobs[0].prompt_past;

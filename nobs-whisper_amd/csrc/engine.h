@@ -7,7 +7,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/whisper.h"
+#include "../../include/whisper_mi355x.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -163,6 +163,7 @@ struct whisper_state {
     // whisper.h single-clip results (job 0 of the last call) + batch results
     std::vector<std::vector<wm::Segment>> results;
     std::vector<int> lang_ids;
+    std::vector<std::vector<whisper_mi355x_window_decision>> decisions;  // per job, per window
     std::vector<int> prompt_past;  // persists across whisper_full calls on this state
     std::mt19937 rng{0};           // decoder 0's rng: created with the state, never reset
     int lang_id = 0;

@@ -75,11 +75,13 @@ struct Reader {
     }
 };
 
+// Host images of the device tensors. A rank that receives its weights by RCCL broadcast
+// (load_weights = false) records sizes only: no host conversion, no H2D copy.
 struct Arena {
-    size_t off = 0;
-    std::vector<std::pair<void**, std::vector<char>>> items;  // target pointer, host bytes
-    void add(void** target, std::vector<char>&& bytes) {
-        items.emplace_back(target, std::move(bytes));
+    struct Item { void** target; size_t size; std::vector<char> bytes; };
+    std::vector<Item> items;
+    void add(void** target, size_t size, std::vector<char>&& bytes) {
+        items.push_back({target, size, std::move(bytes)});
     }
 };
 
@@ -199,7 +201,9 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     const size_t esz = 2;
     auto mat = [&](void** dst, const std::vector<const TensorRef*>& parts, long rows_total, long cols,
                    const std::vector<long>& rows_each, bool conv_reorder, int taps_in) {
-        std::vector<char> b((size_t)rows_total * cols * esz);
+        const size_t sz = (size_t)rows_total * cols * esz;
+        if (!load_weights) { A.add(dst, sz, {}); return; }
+        std::vector<char> b(sz);
         uint16_t* o = (uint16_t*)b.data();
         long row0 = 0;
         for (size_t pi = 0; pi < parts.size(); pi++) {
@@ -225,11 +229,12 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
                 }
             row0 += nr;
         }
-        A.add(dst, std::move(b));
+        A.add(dst, sz, std::move(b));
     };
     auto vecf = [&](float** dst, const std::vector<const TensorRef*>& parts, const std::vector<long>& n_each) {
         long tot = 0;
         for (long x : n_each) tot += x;
+        if (!load_weights) { A.add((void**)dst, tot * 4, {}); return; }
         std::vector<char> b(tot * 4);
         float* o = (float*)b.data();
         long off = 0;
@@ -237,7 +242,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
             for (long i = 0; i < n_each[pi]; i++) o[off + i] = parts[pi] ? elem(*parts[pi], i) : 0.0f;
             off += n_each[pi];
         }
-        A.add((void**)dst, std::move(b));
+        A.add((void**)dst, tot * 4, std::move(b));
     };
     Weights& W = c->w;
     bool ok = true;
@@ -322,9 +327,10 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         // cross K weights per head, transposed: wkT[l][h][c][j] = Wk_l[h*64 + j][c], the B operand of
         // the Q' projection Q'_h = s * Wk_h^T q_h (kernels/xattn.hip)
         const int H = hp.n_text_head;
-        std::vector<char> b((size_t)Ld * H * d * 64 * esz);
+        const size_t sz = (size_t)Ld * H * d * 64 * esz;
+        std::vector<char> b(load_weights ? sz : 0);
         uint16_t* o = (uint16_t*)b.data();
-        for (int l = 0; l < Ld; l++) {
+        for (int l = 0; l < Ld && load_weights; l++) {
             const TensorRef* t = xkv[2 * l];
             for (int h = 0; h < H; h++)
                 for (int j = 0; j < 64; j++)
@@ -340,7 +346,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
                         o[(((size_t)l * H + h) * d + k) * 64 + j] = out;
                     }
         }
-        A.add(&W.wkT, std::move(b));
+        A.add(&W.wkT, sz, std::move(b));
     }
     // mel tables (identical libm expressions to whisper.cpp's whisper_global_cache) + filters^T
     {
@@ -352,12 +358,12 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
             f[400 + i] = cosf(theta);
         }
         for (int i = 0; i < 400; i++) f[800 + i] = 0.5 * (1.0 - cosf((2.0 * M_PI * i) / (400 + 0)));
-        A.add(&W.mel_tab, std::move(b));
+        A.add(&W.mel_tab, b.size(), std::move(b));
         std::vector<char> ft(201 * nm * 4);
         float* o = (float*)ft.data();
         for (int j = 0; j < nm; j++)
             for (int k = 0; k < 201; k++) o[k * nm + j] = c->filters[j * 201 + k];
-        A.add((void**)&W.filt_t, std::move(ft));
+        A.add((void**)&W.filt_t, ft.size(), std::move(ft));
     }
     munmap(map, fsize);
     // ---- one arena, 256-B aligned sub-allocations ------------------------------------------
@@ -365,16 +371,16 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     std::vector<size_t> offs;
     for (auto& it : A.items) {
         offs.push_back(total);
-        total += (it.second.size() + 255) & ~(size_t)255;
+        total += (it.size + 255) & ~(size_t)255;
     }
     WM_CHECK(hipSetDevice(device));
     init_gelu_table();
     WM_CHECK(hipMalloc((void**)&c->arena, total));
     c->arena_bytes = total;
     for (size_t i = 0; i < A.items.size(); i++) {
-        *A.items[i].first = c->arena + offs[i];
-        if (load_weights)
-            WM_CHECK(hipMemcpy(c->arena + offs[i], A.items[i].second.data(), A.items[i].second.size(), hipMemcpyHostToDevice));
+        *A.items[i].target = c->arena + offs[i];
+        if (!A.items[i].bytes.empty())
+            WM_CHECK(hipMemcpy(c->arena + offs[i], A.items[i].bytes.data(), A.items[i].size, hipMemcpyHostToDevice));
     }
     return true;
 }

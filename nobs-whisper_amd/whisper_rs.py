@@ -15,6 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libwhisper_mi355x.so")
 ENGINE_LIB_PATH = os.path.join(HERE, "lib", "libnobs_whisper_engine.so")
 
+# The app's default custom vocabulary (src-tauri/src/config.rs:40-42): the initial prompt of every
+# transcribe call (whisper.rs:98-109, state.rs:276-279) unless the user edits the config file.
+DEFAULT_VOCABULARY = (
+    "Claude Code, Anthropic, Supabase, Vercel, shadcn, tRPC, Drizzle, Zod, pnpm, Bun, Deno, Turso, Neon, "
+    "PlanetScale, Turborepo, Tauri, SvelteKit, Nuxt, Astro, Vite, Zustand, TanStack, LangChain, LlamaIndex, "
+    "Ollama, Cursor, Neovim, Vitest, Playwright, Prisma, Radix, Fly.io, Railway, Cloudflare Workers, Hono, htmx, "
+    "Biome, oxlint, Rspack, Turbopack, Qwik, SolidJS, Convex, Upstash, Resend, Inngest, Replit, v0, Lovable, Bolt, "
+    "WindSurf, Codeium, Supermaven, Aider, OpenRouter, Perplexity, Groq, Mistral, Cohere, Replicate")
+
 F16, BF16 = 0, 1
 FP8_ENC = 2  # bf16 with the encoder QKV/FC1/FC2 GEMMs in fp8 e4m3 (large-v3-turbo fp8 config)
 GREEDY, BEAM_SEARCH = 0, 1
@@ -79,6 +88,13 @@ class TokenData(C.Structure):
                 ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64), ("t_dtw", C.c_int64), ("vlen", C.c_float)]
 
 
+class WindowDecision(C.Structure):
+    """struct whisper_mi355x_window_decision (include/whisper_mi355x.h)."""
+    _fields_ = [("seek", C.c_int32), ("temp_idx", C.c_int32), ("failed0", C.c_int32), ("logprob_fail0", C.c_int32),
+                ("result_len0", C.c_int32), ("no_speech", C.c_int32), ("avg_logprob0", C.c_float),
+                ("entropy0", C.c_float), ("no_speech_prob", C.c_float), ("pad", C.c_float)]
+
+
 _lib = None
 
 
@@ -114,6 +130,12 @@ def lib() -> C.CDLL:
         "whisper_tokenize": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
         "whisper_lang_auto_detect_with_state": (C.c_int, [vp, vp, C.c_int, C.c_int, fp]),
         "whisper_n_vocab": (C.c_int, [vp]),
+        "whisper_is_multilingual": (C.c_int, [vp]),
+        "whisper_model_n_vocab": (C.c_int, [vp]),
+        "whisper_model_n_audio_state": (C.c_int, [vp]),
+        "whisper_model_n_audio_layer": (C.c_int, [vp]),
+        "whisper_model_n_text_layer": (C.c_int, [vp]),
+        "whisper_model_n_mels": (C.c_int, [vp]),
         "whisper_token_sot": (C.c_int, [vp]),
         "whisper_token_eot": (C.c_int, [vp]),
         "whisper_token_beg": (C.c_int, [vp]),
@@ -130,6 +152,7 @@ def lib() -> C.CDLL:
         "whisper_mi355x_batch_token_data": (TokenData, [vp, C.c_int, C.c_int, C.c_int]),
         "whisper_mi355x_batch_lang_id": (C.c_int, [vp, C.c_int]),
         "whisper_mi355x_batch_decoded_tokens": (C.c_long, [vp]),
+        "whisper_mi355x_window_decisions": (C.c_int, [vp, C.c_int, C.POINTER(WindowDecision), C.c_int]),
         "whisper_mi355x_phase_ms": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "whisper_mi355x_get_mel": (C.c_int, [vp, fp, C.c_int]),
         "whisper_mi355x_get_encoder_out": (C.c_int, [vp, fp, C.c_int]),
@@ -284,6 +307,13 @@ class WhisperState:
                                L.whisper_mi355x_batch_segment_t1(self.ptr, job, i),
                                L.whisper_mi355x_batch_segment_text(self.ptr, job, i), toks))
         return out
+
+    def decisions(self, job: int = 0) -> list:
+        """Per-window temperature-fallback decisions of the last full (job 0) / full_batch call."""
+        buf = (WindowDecision * 256)()
+        n = self.L.whisper_mi355x_window_decisions(self.ptr, job, buf, 256)
+        assert n >= 0, n
+        return [{f: getattr(d, f) for f, _ in WindowDecision._fields_ if f != "pad"} for d in buf[:n]]
 
     def phase_ms(self):
         out = (C.c_double * 5)()

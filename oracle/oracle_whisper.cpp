@@ -386,8 +386,11 @@ struct State {
     std::vector<int> prompt_past;
     int lang_id = 0;
     float no_speech_prob = 0.0f;
-    // diagnostics for tests: per decoded step the top-2 prob gap of the greedy choice
+    // diagnostics for tests: per greedy step the top-2 log-probability gap of the chosen token
     std::vector<float> step_margin;
+    // per decoded window: the temperature-fallback decisions (the record whisper_mi355x.h exposes)
+    struct Decision { int seek, temp_idx, failed0, logprob_fail0, result_len0, no_speech; float avg_logprob0, entropy0, no_speech_prob, pad; };
+    std::vector<Decision> decisions;
 };
 
 static void compute_cross(Model& m, State& s) {
@@ -619,7 +622,8 @@ static TokenData sample_token(Model& m, State& s, Decoder& dec, bool best) {
             if (r.p < probs[i]) { second = r.p; r.id = i; r.p = probs[i]; r.plog = dec.logprobs[i]; }
             else if (second < probs[i]) second = probs[i];
         }
-        s.step_margin.push_back(r.p - second);
+        // top-2 log-probability gap of the greedy choice (how far an argmax is from flipping)
+        s.step_margin.push_back(second > 0.0f ? logf(r.p) - logf(second) : 1e9f);
     } else {
         std::discrete_distribution<> dist(probs.begin(), probs.end());
         r.id = dist(dec.rng);
@@ -668,6 +672,7 @@ static int lang_auto_detect(Model& m, State& s) {
 static int full(Model& m, State& s, OracleParams p, const float* samples, int n_samples) {
     s.result.clear();
     s.step_margin.clear();
+    s.decisions.clear();
     if (n_samples > 0) s.n_len = mel_compute(samples, n_samples, m.filters.data(), m.filt_n_mel, m.filt_n_fft, s.mel, &s.n_len_org, m.n_threads);
     const Vocab& vocab = m.vocab;
     std::string lang_str;
@@ -683,8 +688,8 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
     std::vector<float> temperatures;
     if (p.temperature_inc > 0.0f && p.fixed_tokens <= 0)
         for (float t = p.temperature; t < 1.0f + 1e-6f; t += p.temperature_inc) temperatures.push_back(t);
-    else temperatures.push_back(p.temperature);
-    if (p.best_of > 1) return -100;  // only the reference's Greedy{best_of:1}
+    if (temperatures.empty()) temperatures.push_back(p.temperature);
+    // best_of only affects sampled (t > 0) attempts; one candidate is sampled (Greedy{best_of:1})
     auto& prompt_past = s.prompt_past;
     if (p.no_context) prompt_past.clear();
     if (p.initial_prompt) {
@@ -717,6 +722,8 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
         encode(m, s.mel, s.n_len, seek, s.enc);
         compute_cross(m, s);
         if (seek > seek_start && seek + 500 >= seek_end) prompt_past.clear();
+        State::Decision dn{};
+        dn.seek = seek;
         for (int it = 0; it < (int)temperatures.size(); ++it) {
             const float t_cur = temperatures[it];
             dec.sequence = Sequence();
@@ -779,6 +786,14 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
                 sequence_score(p, dec.sequence);
                 if (dec.sequence.result_len > 32 && dec.sequence.entropy < p.entropy_thold) dec.failed = true;
             }
+            if (it == 0) {
+                dn.failed0 = dec.failed;
+                dn.logprob_fail0 = dec.sequence.avg_logprobs < p.logprob_thold;
+                dn.result_len0 = dec.sequence.result_len;
+                dn.avg_logprob0 = (float)dec.sequence.avg_logprobs;
+                dn.entropy0 = (float)dec.sequence.entropy;
+            }
+            dn.temp_idx = it;
             if (it != (int)temperatures.size() - 1)
                 if (dec.failed || dec.sequence.avg_logprobs < p.logprob_thold) success = false;
             if (success) break;
@@ -788,6 +803,9 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
             const int result_len = dec.sequence.result_len;
             const auto& toks = dec.sequence.tokens;
             const bool is_no_speech = (s.no_speech_prob > p.no_speech_thold && dec.sequence.avg_logprobs < p.logprob_thold);
+            dn.no_speech = is_no_speech;
+            dn.no_speech_prob = s.no_speech_prob;
+            s.decisions.push_back(dn);
             prompt_past.clear();
             if (prompt.front() == vocab.token_prev)
                 prompt_past.insert(prompt_past.end(), prompt.begin() + 1, prompt.end() - prompt_init.size());
@@ -899,6 +917,11 @@ int oracle_segment_n_tokens(void* sp, int i) { return (int)((State*)sp)->result[
 int oracle_segment_token(void* sp, int i, int j) { return ((State*)sp)->result[i].tokens[j].id; }
 int oracle_lang(void* sp) { return ((State*)sp)->lang_id; }
 float oracle_no_speech(void* sp) { return ((State*)sp)->no_speech_prob; }
+int oracle_n_decisions(void* sp) { return (int)((State*)sp)->decisions.size(); }
+void oracle_decisions(void* sp, void* out) {
+    auto& d = ((State*)sp)->decisions;
+    memcpy(out, d.data(), d.size() * sizeof(State::Decision));
+}
 int oracle_n_steps(void* sp) { return (int)((State*)sp)->step_margin.size(); }
 void oracle_step_margins(void* sp, float* out) { auto& v = ((State*)sp)->step_margin; std::copy(v.begin(), v.end(), out); }
 // last decoder attempt's full token list (ids) before result_len truncation is not kept; expose the final

@@ -15,6 +15,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "liboracle.so")
 
 
+class Decision(C.Structure):
+    """State::Decision == struct whisper_mi355x_window_decision (include/whisper_mi355x.h)."""
+    _fields_ = [("seek", C.c_int32), ("temp_idx", C.c_int32), ("failed0", C.c_int32), ("logprob_fail0", C.c_int32),
+                ("result_len0", C.c_int32), ("no_speech", C.c_int32), ("avg_logprob0", C.c_float),
+                ("entropy0", C.c_float), ("no_speech_prob", C.c_float), ("pad", C.c_float)]
+
+
+def decisions_to_dicts(arr) -> list:
+    return [{f: getattr(d, f) for f, _ in Decision._fields_ if f != "pad"} for d in arr]
+
+
 class OracleParams(C.Structure):
     _fields_ = [
         ("language", C.c_char_p), ("initial_prompt", C.c_char_p),
@@ -85,6 +96,8 @@ def lib():
             "oracle_lang": (C.c_int, [vp]),
             "oracle_no_speech": (C.c_float, [vp]),
             "oracle_n_steps": (C.c_int, [vp]),
+            "oracle_n_decisions": (C.c_int, [vp]),
+            "oracle_decisions": (None, [vp, vp]),
             "oracle_step_margins": (None, [vp, fp]),
             "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
             "oracle_mel_tables": (None, [fp, fp, fp]),
@@ -188,5 +201,9 @@ class Oracle:
         n = self.L.oracle_n_steps(self.s)
         margins = np.empty(n, np.float32)
         self.L.oracle_step_margins(self.s, _fp(margins))
+        nd = self.L.oracle_n_decisions(self.s)
+        dec = (Decision * max(1, nd))()
+        self.L.oracle_decisions(self.s, C.cast(dec, C.c_void_p))
         return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
-                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins)
+                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins,
+                    decisions=decisions_to_dicts(dec[:nd]))

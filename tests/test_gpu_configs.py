@@ -1,0 +1,313 @@
+"""GPU parity on every BASELINE.json config shape (VERDICT r1 "next" #2).
+
+Each config keeps its real dimensions (n_mels, d, heads, n_vocab) at reduced depth where the CPU
+oracle would otherwise take minutes (tools/make_model.py SHAPES):
+  tiny.en  -> tiny.en (4+4 layers, V 51864, English-only special ids)
+  base     -> base (6+6 layers, full depth), f16, B = 1
+  small    -> small-4L (d 768, 12 heads, 4+4 layers), bf16, B = 2 vs the oracle, B = 32 batch == single
+  large-v3 -> large-v3-2L (128 mels, d 1280, 20 heads, V 51866, 2+2 layers), f16 and bf16
+  turbo    -> large-v3-turbo-2L (large-v3 dims, 2 encoder + 4 decoder layers), fp8 encoder vs bf16
+All use the "+conf" weights (make_model.CONF_SCALE): a decoder as peaked as a trained one, so the
+reference's FullParams (whisper.rs:88-124, temperature_inc 0.2) succeed at t = 0 on most windows and
+the comparison covers the path the app actually takes (no sampled fallback).
+
+Bars (integer outputs exact, as the north star asks for f16):
+  * mel: bit-exact, 80 and 128 mels;
+  * encoder output: f16 <= 3e-2 max abs / 3e-3 mean abs; bf16 <= 0.25 max / 2.5e-2 mean abs (LN
+    outputs of O(1); bf16 keeps 8 mantissa bits);
+  * whisper_full, f16: token ids, timestamps, segment text and the per-window fallback decisions
+    identical to the oracle, in both cross-attention modes (direct from E, and the cross-KV cache);
+  * whisper_full, bf16: token ids identical to the f16-numerics oracle on every step whose greedy
+    choice leads the runner-up by more than BF16_GAP nats of log-probability (the oracle's
+    per-step margin); comparison stops at the first closer step.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from make_model import synthetic_pcm
+from oracle_py import Oracle, reference_params
+
+pytestmark = pytest.mark.gpu
+
+BF16_GAP = 0.5  # nats: bf16 logits stay within ~0.15 of the f16 oracle's (test_bf16_argmax_agreement)
+
+_ORACLE = {}
+
+
+def oracle_full(shape, pcm_key, lang, prompt=None, t_inc=0.2):
+    """Cached oracle whisper_full (the CPU restatement is the slow side)."""
+    from conftest import model_path
+    key = (shape, pcm_key, lang, prompt, t_inc)
+    if key not in _ORACLE:
+        o = Oracle(model_path(shape), mode=1, n_threads=16)
+        rp = reference_params(lang, prompt=prompt)
+        rp.temperature_inc = t_inc
+        _ORACLE[key] = o.full(_pcm(pcm_key), rp)
+        o.close()
+    return _ORACLE[key]
+
+
+def _pcm(key):
+    k, sec = key
+    return synthetic_pcm(k, seconds=sec)
+
+
+def gpu_full(wrs, path, dtype, pcm, lang, prompt=None, t_inc=0.2, cross="direct", monkeypatch=None):
+    if monkeypatch is not None:
+        monkeypatch.setenv("WHISPER_MI355X_CROSS", cross)
+    ctx = wrs.WhisperContext(path, dtype=dtype)
+    st = ctx.create_state()
+    gp = wrs.reference_full_params(lang, initial_prompt=prompt)
+    gp.temperature_inc = t_inc
+    assert st.full(gp, pcm) == 0
+    segs = st.segments()
+    dec = st.decisions()
+    lang_id = wrs.lib().whisper_full_lang_id_from_state(st.ptr)
+    st.close()
+    ctx.close()
+    return segs, dec, lang_id
+
+
+def seg_ints(segs):
+    return [([t[0] for t in s.tokens], s.t0, s.t1) for s in segs]
+
+
+def ref_ints(res):
+    return [(s["tokens"], s["t0"], s["t1"]) for s in res["segments"]]
+
+
+DEC_KEYS = ("seek", "temp_idx", "failed0", "logprob_fail0", "result_len0", "no_speech")
+
+
+def dec_ints(ds):
+    return [tuple(d[k] for k in DEC_KEYS) for d in ds]
+
+
+def assert_decisions_match(got, ref):
+    assert dec_ints(got) == dec_ints(ref["decisions"])
+    for g, r in zip(got, ref["decisions"]):
+        if np.isfinite(r["avg_logprob0"]):
+            assert abs(g["avg_logprob0"] - r["avg_logprob0"]) < 2e-3, (g, r)
+        assert abs(g["entropy0"] - r["entropy0"]) < 1e-6, (g, r)
+
+
+def n_mels_of(path):
+    import struct
+    with open(path, "rb") as f:
+        f.read(4)
+        return struct.unpack("<11i", f.read(44))[9]
+
+
+# ---- mel: 80 and 128 bins --------------------------------------------------------------------------
+@pytest.mark.parametrize("shape", ["tiny.en+conf", "large-v3-2L+conf"])
+@pytest.mark.parametrize("seconds", [30.0, 7.3])
+def test_mel_bit_exact_config(wrs, shape, seconds):
+    from conftest import model_path
+    path = model_path(shape)
+    nm = n_mels_of(path)
+    pcm = synthetic_pcm(5, seconds=seconds)
+    ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+    st = ctx.create_state()
+    L = wrs.lib()
+    assert L.whisper_pcm_to_mel_with_state(ctx.ptr, st.ptr, pcm.ctypes.data_as(C.POINTER(C.c_float)), len(pcm), 1) == 0
+    n_len = (len(pcm) + 480000) // 160
+    g = np.empty((nm, n_len), np.float32)
+    assert L.whisper_mi355x_get_mel(st.ptr, g.ctypes.data_as(C.POINTER(C.c_float)), g.size) == n_len
+    st.close(); ctx.close()
+    o = Oracle(path, mode=1, n_threads=16)
+    r, _ = o.mel(pcm)
+    o.close()
+    assert r.shape == (nm, n_len)
+    diff = np.count_nonzero(g.view(np.uint32) != r.view(np.uint32))
+    assert diff == 0, f"{diff} of {g.size} mel values differ (n_mels {nm})"
+
+
+# ---- encoder ----------------------------------------------------------------------------------------
+@pytest.mark.parametrize("shape,dtype,tol_max,tol_mean", [
+    ("tiny.en+conf", "F16", 3e-2, 3e-3), ("base+conf", "F16", 3e-2, 3e-3),
+    ("small-4L+conf", "BF16", 0.25, 2.5e-2), ("large-v3-2L+conf", "F16", 3e-2, 3e-3),
+    ("large-v3-2L+conf", "BF16", 0.25, 2.5e-2)])
+def test_encoder_config(wrs, shape, dtype, tol_max, tol_mean):
+    from conftest import model_path
+    path = model_path(shape)
+    pcm = synthetic_pcm(0)
+    ctx = wrs.WhisperContext(path, dtype=getattr(wrs, dtype))
+    st = ctx.create_state()
+    L = wrs.lib()
+    assert L.whisper_pcm_to_mel_with_state(ctx.ptr, st.ptr, pcm.ctypes.data_as(C.POINTER(C.c_float)), len(pcm), 1) == 0
+    assert L.whisper_encode_with_state(ctx.ptr, st.ptr, 0, 1) == 0
+    d = L.whisper_model_n_audio_state(ctx.ptr)
+    out = np.empty((1500, d), np.float32)
+    assert L.whisper_mi355x_get_encoder_out(st.ptr, out.ctypes.data_as(C.POINTER(C.c_float)), out.size) == 0
+    st.close(); ctx.close()
+    o = Oracle(path, mode=1, n_threads=16)
+    o.mel(pcm)
+    ref = o.encode(0)
+    o.close()
+    err = np.abs(out - ref)
+    assert err.max() < tol_max and err.mean() < tol_mean, (err.max(), err.mean())
+
+
+# ---- whisper_full, f16: exact ------------------------------------------------------------------------
+F16_CASES = [
+    # shape, clip (seed, seconds), language, prompt, temperature_inc. Every case's oracle run decides
+    # each window at t = 0 (asserted), so all its integer outputs are comparable; the one case with
+    # temperature_inc 0 falls back under the verbatim params.
+    ("tiny.en+conf", (0, 30.0), "en", "DEFAULT", 0.2),
+    ("tiny.en+conf", (1, 30.0), None, None, 0.2),
+    ("tiny.en+conf", (1, 30.0), "en", None, 0.0),
+    ("base+conf", (0, 30.0), "en", None, 0.2),
+    ("base+conf", (1, 30.0), "en", "DEFAULT", 0.2),
+    ("large-v3-2L+conf", (0, 30.0), "en", None, 0.2),
+    ("large-v3-2L+conf", (1, 30.0), None, None, 0.2),
+    ("large-v3-2L+conf", (0, 30.0), None, "DEFAULT", 0.2),
+    ("large-v3-turbo-2L+conf", (1, 30.0), "en", None, 0.2),
+]
+
+
+@pytest.mark.parametrize("cross", ["direct", "cache"])
+@pytest.mark.parametrize("shape,clip,lang,prompt,t_inc", F16_CASES)
+def test_full_config_f16_exact(wrs, monkeypatch, cross, shape, clip, lang, prompt, t_inc):
+    from conftest import model_path
+    prompt = wrs.DEFAULT_VOCABULARY if prompt == "DEFAULT" else prompt
+    ref = oracle_full(shape, clip, lang, prompt, t_inc)
+    assert all(d["temp_idx"] == 0 for d in ref["decisions"]), ref["decisions"]
+    segs, dec, lang_id = gpu_full(wrs, model_path(shape), wrs.F16, _pcm(clip), lang, prompt, t_inc=t_inc,
+                                  cross=cross, monkeypatch=monkeypatch)
+    assert_decisions_match(dec, ref)
+    assert seg_ints(segs) == ref_ints(ref)
+    assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
+    if lang is None:
+        assert lang_id == ref["lang"]
+
+
+# ---- whisper_full, bf16: exact on every step the oracle decides by > BF16_GAP nats -------------------
+BF16_CASES = [
+    ("small-4L+conf", (0, 30.0), "en", None),
+    ("small-4L+conf", (1, 30.0), None, None),
+    ("large-v3-2L+conf", (0, 30.0), "en", None),
+    ("large-v3-2L+conf", (1, 30.0), "en", "DEFAULT"),
+    ("large-v3-turbo-2L+conf", (0, 30.0), "en", None),
+]
+
+
+@pytest.mark.parametrize("shape,clip,lang,prompt", BF16_CASES)
+def test_full_config_bf16_margin(wrs, shape, clip, lang, prompt):
+    from conftest import model_path
+    prompt = wrs.DEFAULT_VOCABULARY if prompt == "DEFAULT" else prompt
+    ref = oracle_full(shape, clip, lang, prompt, t_inc=0.0)   # one greedy attempt per window
+    segs, dec, _ = gpu_full(wrs, model_path(shape), wrs.BF16, _pcm(clip), lang, prompt, t_inc=0.0)
+    if len(ref["decisions"]) != 1:
+        pytest.skip("margin gate needs a single-window oracle run")
+    got = [t for s in seg_ints(segs) for t in s[0]]
+    exp = [t for s in ref_ints(ref) for t in s[0]]
+    m = ref["margins"]
+    n = 0
+    while n < len(exp) and n < len(m) and m[n] > BF16_GAP:
+        n += 1
+    assert n >= min(8, len(exp)), f"oracle margins too small to gate: {m[:8]}"
+    assert got[:n] == exp[:n], f"first {n} confidently decided tokens differ"
+
+
+# ---- small bf16, B = 32: batch == single; B = 2 vs the oracle ------------------------------------------
+def test_small_bf16_batch32_equals_single(wrs):
+    from conftest import model_path
+    path = model_path("small-4L+conf")
+    ctx = wrs.WhisperContext(path, dtype=wrs.BF16)
+    clips = [synthetic_pcm(k) for k in range(32)]
+    p = wrs.reference_full_params("en")
+    st = ctx.create_state()
+    assert st.full_batch(p, clips) == 0
+    batch = [seg_ints(st.batch_segments(j)) for j in range(32)]
+    bdec = [dec_ints(st.decisions(j)) for j in range(32)]
+    st.close()
+    for j in (0, 7, 19, 31):  # spot-check singles against the batch
+        st = ctx.create_state()
+        assert st.full(p, clips[j]) == 0
+        assert seg_ints(st.segments()) == batch[j], j
+        assert dec_ints(st.decisions()) == bdec[j], j
+        st.close()
+    ctx.close()
+
+
+def test_small_bf16_batch2_vs_oracle(wrs):
+    """B = 2 through whisper_mi355x_full_batch, each clip's confidently-decided tokens vs the oracle."""
+    from conftest import model_path
+    path = model_path("small-4L+conf")
+    ctx = wrs.WhisperContext(path, dtype=wrs.BF16)
+    st = ctx.create_state()
+    p = wrs.reference_full_params("en")
+    p.temperature_inc = 0.0
+    assert st.full_batch(p, [synthetic_pcm(0), synthetic_pcm(1)]) == 0
+    for j in range(2):
+        ref = oracle_full("small-4L+conf", (j, 30.0), "en", None, t_inc=0.0)
+        got = [t for s in seg_ints(st.batch_segments(j)) for t in s[0]]
+        exp = [t for s in ref_ints(ref) for t in s[0]]
+        m = ref["margins"]
+        n = 0
+        while n < len(exp) and n < len(m) and m[n] > BF16_GAP:
+            n += 1
+        assert got[:n] == exp[:n], j
+    st.close(); ctx.close()
+
+
+# ---- turbo: fp8 encoder against the bf16 encoder -------------------------------------------------------
+def test_turbo_fp8_encoder_vs_bf16(wrs):
+    from conftest import model_path
+    path = model_path("large-v3-turbo-2L+conf")
+    pcm = synthetic_pcm(0)
+    L = wrs.lib()
+    outs = {}
+    for name, dt in (("bf16", wrs.BF16), ("fp8", wrs.FP8_ENC)):
+        ctx = wrs.WhisperContext(path, dtype=dt)
+        st = ctx.create_state()
+        assert L.whisper_pcm_to_mel_with_state(ctx.ptr, st.ptr, pcm.ctypes.data_as(C.POINTER(C.c_float)), len(pcm), 1) == 0
+        assert L.whisper_encode_with_state(ctx.ptr, st.ptr, 0, 1) == 0
+        out = np.empty((1500, 1280), np.float32)
+        assert L.whisper_mi355x_get_encoder_out(st.ptr, out.ctypes.data_as(C.POINTER(C.c_float)), out.size) == 0
+        outs[name] = out
+        st.close(); ctx.close()
+    a, b = outs["fp8"], outs["bf16"]
+    rel = np.sqrt(((a - b) ** 2).mean() / (b ** 2).mean())
+    cos = (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+    assert rel < 0.08 and cos.min() > 0.99, (rel, cos.min())
+
+
+# ---- temperature fallback: the comparable integer decisions ---------------------------------------------
+@pytest.mark.parametrize("shape,t_inc", [("micro", 0.2), ("tiny", 0.2), ("tiny+conf", 0.2), ("micro", 0.0)])
+def test_fallback_decisions_match_oracle(wrs, shape, t_inc):
+    """Per window: the t = 0 attempt's failed / avg_logprob / entropy outcome, its result_len, and
+    whether the window fell back, equal the oracle's (reference thresholds whisper.rs:122-124).
+    Once a window's final attempt is sampled (t > 0), std::discrete_distribution over device vs host
+    probabilities may draw differently: later windows are compared only while the
+    sampled tokens agree."""
+    from conftest import model_path
+    ref = oracle_full(shape, (0, 30.0), "en", None, t_inc=t_inc)
+    segs, dec, _ = gpu_full(wrs, model_path(shape), wrs.F16, _pcm((0, 30.0)), "en", None, t_inc=t_inc)
+    rd = ref["decisions"]
+    assert len(dec) >= 1 and len(rd) >= 1
+    # window 0's greedy attempt is always comparable
+    first = ("seek", "failed0", "logprob_fail0", "result_len0")
+    assert tuple(dec[0][k] for k in first) == tuple(rd[0][k] for k in first)
+    assert (dec[0]["temp_idx"] > 0) == (rd[0]["temp_idx"] > 0)
+    if rd[0]["temp_idx"] == 0 or seg_ints(segs) == ref_ints(ref):
+        assert_decisions_match(dec, ref)
+
+
+# ---- long-form (> 30 s): the seek loop with prompt carry-over -------------------------------------------
+@pytest.mark.parametrize("cross", ["direct", "cache"])
+@pytest.mark.parametrize("clip", [(2, 70.0), (3, 45.5)])
+def test_long_form_matches_oracle(wrs, monkeypatch, cross, clip):
+    """whisper_full over a > 30 s clip (state.rs:757-778 hands such remainders to one call when no
+    silence split is found, audio.rs:474-507): several 30 s windows, each prompted with the previous
+    window's tokens (<|startofprev|> + prompt_past). temperature_inc = 0: greedy windows only."""
+    from conftest import model_path
+    ref = oracle_full("tiny+conf", clip, "en", None, t_inc=0.0)
+    assert len(ref["decisions"]) >= 2
+    segs, dec, _ = gpu_full(wrs, model_path("tiny+conf"), wrs.F16, _pcm(clip), "en", None, t_inc=0.0, cross=cross,
+                            monkeypatch=monkeypatch)
+    assert_decisions_match(dec, ref)
+    assert seg_ints(segs) == ref_ints(ref)
+    assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]

@@ -38,7 +38,28 @@ SHAPES = {
     "medium":   (51865, 80, 1024, 16, 24, 24),
     "large-v3": (51866, 128, 1280, 20, 32, 32),
     "large-v3-turbo": (51866, 128, 1280, 20, 32, 4),
+    # BASELINE config shapes at reduced depth (real d / heads / n_mels / n_vocab), so that the CPU
+    # oracle runs a whole whisper_full in seconds inside the parity tests
+    "small-4L": (51865, 80, 768, 12, 4, 4),
+    "large-v3-2L": (51866, 128, 1280, 20, 2, 2),
+    "large-v3-turbo-2L": (51866, 128, 1280, 20, 2, 4),
 }
+
+# "+conf" variant: a decoder whose output distribution is as peaked as a trained model's (random
+# weights give near-flat logits, avg logprob ~ -6, so every window falls back to sampled t > 0
+# attempts). decoder.ln is scaled (logit std ~ CONF_SCALE), column 0 of the final LN output is a
+# constant 1 and the timestamp rows of the token embedding carry CONF_TS_BOOST there (timestamps
+# compete with text, so windows end on timestamp pairs), and the decoder positional embedding is
+# CONF_POS_SCALE x larger (the greedy sequence does not cycle, entropy stays above 2.4). With the
+# reference's FullParams the greedy t = 0 attempt then passes the fallback thresholds.
+CONF_SCALE, CONF_TS_BOOST, CONF_POS_SCALE = 6.0, 14.0, 10.0
+
+
+def token_beg(n_vocab: int) -> int:
+    """whisper.cpp's token_beg for a vocabulary size (special ids shift in multilingual files)."""
+    if n_vocab < 51865:
+        return 50363
+    return 50363 + (n_vocab - 51765 - 1) - 98
 
 N_AUDIO_CTX = 1500
 N_TEXT_CTX = 448
@@ -203,9 +224,23 @@ def init_tensor(rng, name, shape, d, n_mels):
     return (std * rng.standard_normal(shape, dtype=np.float32)).astype(np.float32)
 
 
+def conf_adjust(name: str, t: np.ndarray, n_vocab: int) -> np.ndarray:
+    if name in ("decoder.ln.weight", "decoder.ln.bias"):
+        t = t * CONF_SCALE
+        t[0] = 0.0 if name.endswith("weight") else 1.0
+    elif name == "decoder.token_embedding.weight":
+        t[:, 0] = 0.0
+        t[token_beg(n_vocab):, 0] = CONF_TS_BOOST
+    elif name == "decoder.positional_embedding":
+        t = t * CONF_POS_SCALE
+    return t
+
+
 def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1) -> dict:
-    """Write a seeded synthetic model. Returns the hparams dict. ftype 1 = f16 matrices, 0 = all f32."""
-    n_vocab, n_mels, d, h, n_enc, n_dec = SHAPES[shape]
+    """Write a seeded synthetic model. Returns the hparams dict. ftype 1 = f16 matrices, 0 = all f32.
+    shape may carry the "+conf" suffix (see CONF_SCALE)."""
+    conf = shape.endswith("+conf")
+    n_vocab, n_mels, d, h, n_enc, n_dec = SHAPES[shape[:-5] if conf else shape]
     rng = np.random.default_rng(seed)
     hp = dict(n_vocab=n_vocab, n_audio_ctx=N_AUDIO_CTX, n_audio_state=d, n_audio_head=h,
               n_audio_layer=n_enc, n_text_ctx=N_TEXT_CTX, n_text_state=d, n_text_head=h,
@@ -224,6 +259,8 @@ def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1) -
             f.write(t)
         for name, shp, is_f32 in tensor_specs(n_vocab, n_mels, d, n_enc, n_dec):
             data = init_tensor(rng, name, shp, d, n_mels)
+            if conf:
+                data = conf_adjust(name, data, n_vocab)
             use_f16 = (ftype == 1) and not is_f32
             nb = name.encode()
             f.write(struct.pack("<3i", len(shp), len(nb), 1 if use_f16 else 0))
@@ -268,7 +305,7 @@ def synthetic_pcm(k: int, seconds: float = 30.0, sr: int = 16000) -> np.ndarray:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
-    ap.add_argument("--shape", default="tiny", choices=sorted(SHAPES))
+    ap.add_argument("--shape", default="tiny", choices=sorted(SHAPES) + [k + "+conf" for k in sorted(SHAPES)])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--ftype", type=int, default=1)
     a = ap.parse_args()
