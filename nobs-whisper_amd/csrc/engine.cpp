@@ -1233,6 +1233,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
     s->decoded_tokens = S.decoded;
     s->phase_ms[0] = S.t_mel; s->phase_ms[1] = S.t_enc; s->phase_ms[2] = S.t_prefill; s->phase_ms[3] = S.t_decode;
     s->phase_ms[4] = S.t_logits;
+    std::lock_guard<std::mutex> lk(c->timings_mu);
     c->timings.encode_ms += (float)S.t_enc;
     c->timings.decode_ms += (float)S.t_decode;
     c->timings.prompt_ms += (float)S.t_prefill;

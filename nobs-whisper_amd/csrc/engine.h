@@ -74,6 +74,7 @@ struct Context {
     char* arena = nullptr;
     size_t arena_bytes = 0;
     whisper_timings timings{};
+    std::mutex timings_mu;  // states on different threads add their phase times here
     whisper_state* default_state = nullptr;  // whisper_init_from_file_with_params (with state)
     float k_scale = 0.0f;                    // d_head^-0.25
     // Cross attention straight from the encoder output (kernels/xattn.hip) instead of through a

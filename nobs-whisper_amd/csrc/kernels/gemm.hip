@@ -17,6 +17,7 @@
 //
 // Roofline: MFMA-bound for the encoder/cross-KV/prefill shapes (M = B*1500), HBM-bound on the
 // weights for decode steps (M = number of active sequences).
+#include <mutex>
 #include "../common.h"
 #include "../kernels.h"
 
@@ -37,6 +38,8 @@ __device__ uint16_t g_gelu_tab[65536];
 
 void init_gelu_table() {
     static std::vector<uint16_t> tab;
+    static std::mutex mu;  // contexts may be created from several threads
+    std::lock_guard<std::mutex> lk(mu);
     if (tab.empty()) {
         tab.resize(65536);
         const float GELU_COEF_A = 0.044715f;
@@ -1303,6 +1306,7 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     else gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
     return splits;
 }
+
 
 int launch_gemm_partials(DType dt, const GemmArgs& g, hipStream_t st) {
     return dt == DType::F16 ? launch_partials_t<half_t>(g, st) : launch_partials_t<bf16_t>(g, st);

@@ -78,6 +78,52 @@ const char* const kHallucinationPhrases[] = {  // whisper.rs:202-230
     "MBC \xeb\x89\xb4\xec\x8a\xa4 \xec\x9d\xb4\xeb\x8d\x95\xec\x98\x81\xec\x9e\x85\xeb\x8b\x88\xeb\x8b\xa4",
 };
 
+}  // namespace
+
+// String::from_utf8_lossy (what whisper-rs's WhisperSegment::to_str_lossy returns, whisper.rs:137):
+// every maximal ill-formed subsequence (Unicode "substitution of maximal subparts") becomes one
+// U+FFFD, valid sequences are copied.
+std::string utf8_lossy(const std::string& in) {
+    std::string out;
+    const size_t n = in.size();
+    auto b = [&](size_t i) { return (unsigned char)in[i]; };
+    for (size_t i = 0; i < n;) {
+        const unsigned char c = b(i);
+        if (c < 0x80) { out += (char)c; i++; continue; }
+        int len = 0;
+        unsigned char lo = 0x80, hi = 0xbf;  // allowed range of the second byte
+        if (c >= 0xc2 && c <= 0xdf) len = 2;
+        else if (c == 0xe0) { len = 3; lo = 0xa0; }
+        else if ((c >= 0xe1 && c <= 0xec) || c == 0xee || c == 0xef) len = 3;
+        else if (c == 0xed) { len = 3; hi = 0x9f; }
+        else if (c == 0xf0) { len = 4; lo = 0x90; }
+        else if (c >= 0xf1 && c <= 0xf3) len = 4;
+        else if (c == 0xf4) { len = 4; hi = 0x8f; }
+        if (len == 0) { out += "\xef\xbf\xbd"; i++; continue; }
+        size_t k = 1;
+        for (; k < (size_t)len && i + k < n; k++) {
+            const unsigned char x = b(i + k);
+            const bool ok = k == 1 ? (x >= lo && x <= hi) : (x >= 0x80 && x <= 0xbf);
+            if (!ok) break;
+        }
+        if (k == (size_t)len) out.append(in, i, len);
+        else out += "\xef\xbf\xbd";
+        i += k;
+    }
+    return out;
+}
+
+// initial_prompt of whisper.rs:98-105: "{vocab} {ctx}" / vocab / ctx / none
+bool build_initial_prompt(const char* vocabulary, const char* context, std::string* out) {
+    const bool has_vocab = vocabulary != nullptr, has_ctx = context != nullptr;
+    if (has_vocab && has_ctx && vocabulary[0] != '\0') { *out = std::string(vocabulary) + " " + context; return true; }
+    if (has_vocab && !has_ctx && vocabulary[0] != '\0') { *out = vocabulary; return true; }
+    if (has_ctx) { *out = context; return true; }
+    return false;
+}
+
+namespace {
+
 std::string trim(const std::string& s) {
     auto cp = decode_utf8(s);
     size_t b = 0, e = cp.size();
@@ -149,13 +195,8 @@ WhisperError WhisperEngine::transcribe(const float* audio, size_t n, const char*
     whisper_full_params params = whisper_full_default_params(WHISPER_SAMPLING_GREEDY);  // whisper.rs:88
     params.greedy.best_of = 1;
     params.language = language;  // None => NULL => auto-detect (whisper.rs:91-95)
-    std::string prompt;          // whisper.rs:98-105
-    bool have_prompt = false;
-    const bool has_vocab = vocabulary != nullptr, has_ctx = context != nullptr;
-    if (has_vocab && has_ctx && vocabulary[0] != '\0') { prompt = std::string(vocabulary) + " " + context; have_prompt = true; }
-    else if (has_vocab && !has_ctx && vocabulary[0] != '\0') { prompt = vocabulary; have_prompt = true; }
-    else if (has_ctx) { prompt = context; have_prompt = true; }
-    if (have_prompt) params.initial_prompt = prompt.c_str();
+    std::string prompt;  // whisper.rs:98-109
+    if (build_initial_prompt(vocabulary, context, &prompt)) params.initial_prompt = prompt.c_str();
     params.print_special = false;  // whisper.rs:112-124
     params.print_progress = false;
     params.print_realtime = false;
@@ -177,7 +218,7 @@ WhisperError WhisperEngine::transcribe(const float* audio, size_t n, const char*
     const int n_seg = whisper_full_n_segments_from_state(state);
     for (int i = 0; i < n_seg; i++) {
         const char* t = whisper_full_get_segment_text_from_state(state, i);
-        if (t) result += t;
+        if (t) result += utf8_lossy(t);  // per segment, as whisper-rs
     }
     whisper_free_state(state);
     *out = filter_hallucinations(trim(result));  // whisper.rs:143-144
@@ -225,6 +266,31 @@ __attribute__((visibility("default"))) int nobs_engine_transcribe(void* e, const
     if ((int)text.size() + 1 > cap) return -100;
     memcpy(out, text.c_str(), text.size() + 1);
     return (int)text.size();
+}
+__attribute__((visibility("default"))) int nobs_engine_transcribe_chunked(void* e, const float* const* chunks,
+                                                                         const int* n, int n_chunks, const char* lang,
+                                                                         const char* vocab, char* out, int cap) {
+    std::vector<std::vector<float>> cs(n_chunks);
+    for (int i = 0; i < n_chunks; i++) cs[i].assign(chunks[i], chunks[i] + n[i]);
+    std::string text, msg;
+    const auto r = ((nobs::WhisperEngine*)e)->transcribe_chunked(cs, lang, vocab, &text, &msg);
+    if (r != nobs::WhisperError::Ok) return -(int)r;
+    if ((int)text.size() + 1 > cap) return -100;
+    memcpy(out, text.c_str(), text.size() + 1);
+    return (int)text.size();
+}
+__attribute__((visibility("default"))) int nobs_build_initial_prompt(const char* vocab, const char* ctx, char* out, int cap) {
+    std::string p;
+    if (!nobs::build_initial_prompt(vocab, ctx, &p)) return -1;  // None
+    if ((int)p.size() + 1 > cap) return -100;
+    memcpy(out, p.c_str(), p.size() + 1);
+    return (int)p.size();
+}
+__attribute__((visibility("default"))) int nobs_utf8_lossy(const char* in, int n, char* out, int cap) {
+    const std::string r = nobs::utf8_lossy(std::string(in, n));
+    if ((int)r.size() + 1 > cap) return -1;
+    memcpy(out, r.c_str(), r.size() + 1);
+    return (int)r.size();
 }
 __attribute__((visibility("default"))) int nobs_filter_hallucinations(const char* in, char* out, int cap) {
     const std::string r = nobs::filter_hallucinations(in);

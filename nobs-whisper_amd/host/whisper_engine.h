@@ -42,5 +42,9 @@ class WhisperEngine {
 
 // whisper.rs:200-260
 std::string filter_hallucinations(const std::string& text);
+// String::from_utf8_lossy: each maximal ill-formed subsequence -> U+FFFD (segment.to_str_lossy(), whisper.rs:137)
+std::string utf8_lossy(const std::string& bytes);
+// whisper.rs:98-105 initial prompt; false = None
+bool build_initial_prompt(const char* vocabulary, const char* context, std::string* out);
 
 }  // namespace nobs

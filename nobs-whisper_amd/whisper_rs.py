@@ -347,6 +347,8 @@ class WhisperEngine:
         L.nobs_engine_is_loaded.argtypes = [C.c_void_p]
         L.nobs_engine_transcribe.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.c_char_p, C.c_char_p,
                                              C.c_char_p, C.c_char_p, C.c_int]
+        L.nobs_engine_transcribe_chunked.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_int),
+                                                     C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
         self.L = L
         self.ptr = L.nobs_engine_new()
 
@@ -366,11 +368,48 @@ class WhisperEngine:
                                            enc(vocabulary), enc(context), buf, len(buf))
         return (0, buf.value.decode("utf-8", "replace")) if rc >= 0 else (rc, None)
 
+    def transcribe_chunked(self, chunks, language=None, vocabulary=None):
+        """whisper.rs:152-197: sequential transcribe calls, each prompted with the previous non-empty
+        result; results joined with a space. Returns (rc, text)."""
+        import numpy as np
+        arrs = [np.ascontiguousarray(c, dtype=np.float32) for c in chunks]
+        ptrs = (C.POINTER(C.c_float) * len(arrs))(*[a.ctypes.data_as(C.POINTER(C.c_float)) for a in arrs])
+        lens = (C.c_int * len(arrs))(*[len(a) for a in arrs])
+        buf = C.create_string_buffer(1 << 20)
+        enc = lambda s: s.encode() if s is not None else None  # noqa: E731
+        rc = self.L.nobs_engine_transcribe_chunked(self.ptr, ptrs, lens, len(arrs), enc(language), enc(vocabulary),
+                                                   buf, len(buf))
+        return (0, buf.value.decode("utf-8", "replace")) if rc >= 0 else (rc, None)
+
     def __del__(self):
         try:
             self.L.nobs_engine_free(self.ptr)
         except Exception:
             pass
+
+
+def _engine_lib():
+    return C.CDLL(ENGINE_LIB_PATH)
+
+
+def build_initial_prompt(vocabulary, context):
+    """whisper.rs:98-105 through the C++ mirror: None when the match falls through."""
+    L = _engine_lib()
+    L.nobs_build_initial_prompt.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+    buf = C.create_string_buffer(1 << 16)
+    enc = lambda s: s.encode() if s is not None else None  # noqa: E731
+    n = L.nobs_build_initial_prompt(enc(vocabulary), enc(context), buf, len(buf))
+    return None if n == -1 else buf.value.decode()
+
+
+def utf8_lossy(data: bytes) -> bytes:
+    """The mirror's String::from_utf8_lossy (segment.to_str_lossy, whisper.rs:137)."""
+    L = _engine_lib()
+    L.nobs_utf8_lossy.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int]
+    buf = C.create_string_buffer(3 * len(data) + 16)
+    n = L.nobs_utf8_lossy(data, len(data), buf, len(buf))
+    assert n >= 0
+    return buf.raw[:n]
 
 
 def filter_hallucinations(text: str) -> str:

@@ -134,6 +134,12 @@ class Oracle:
         (self.n_vocab, self.n_audio_ctx, self.d, self.n_head, self.n_enc, self.n_text_ctx, _, _,
          self.n_dec, self.n_mels, _) = hp
 
+    def new_state(self):
+        """A fresh whisper_state (whisper.rs:83-85 creates one per transcribe call): empty
+        prompt_past, rng re-seeded."""
+        self.L.oracle_state_free(self.s)
+        self.s = self.L.oracle_state_new(self.m)
+
     def close(self):
         if self.m:
             self.L.oracle_state_free(self.s)

@@ -41,3 +41,33 @@ def test_transcribe_without_model(wrs):
     e = wrs.WhisperEngine()
     rc, text = e.transcribe(np.zeros(16000, np.float32))
     assert rc == wrs.WhisperEngine.NO_MODEL and text is None
+
+
+@pytest.mark.parametrize("vocab,ctx,expected", [
+    ("Claude Code, Anthropic", "previous text", "Claude Code, Anthropic previous text"),  # (Some(v), Some(c)) if !v.is_empty()
+    ("Claude Code, Anthropic", None, "Claude Code, Anthropic"),                           # (Some(v), None) if !v.is_empty()
+    (None, "previous text", "previous text"),                                             # (_, Some(c))
+    ("", "previous text", "previous text"),                                               # empty vocab falls to (_, Some(c))
+    ("", None, None),                                                                     # _ => None
+    (None, None, None),
+    ("vocab", "", "vocab "),                                                              # Some("") context is still Some
+])
+def test_initial_prompt_branches(wrs, vocab, ctx, expected):
+    """whisper.rs:98-105: the four match arms of the initial-prompt assembly."""
+    assert wrs.build_initial_prompt(vocab, ctx) == expected
+
+
+def test_utf8_lossy_matches_rust_semantics(wrs):
+    """segment.to_str_lossy() (whisper.rs:137) is String::from_utf8_lossy: each maximal ill-formed
+    subsequence becomes one U+FFFD. Python's 'replace' handler implements the same Unicode
+    practice, so it is the reference here (fuzzed over segment-edge splits of multi-byte chars)."""
+    import random
+    rng = random.Random(0)
+    pieces = [b"\xe2\x82", b"\xf0\x9f\x98\x80", b"\xed\xa0\x80", b"\xc0\xaf", b"\xf4\x90\x80\x80", b"a", b" ",
+              b"\xe6\x84\x9f", b"\x80", b"\xff", b"\xf0\x80\x80", b"\xe0\x80\xaf", b"\xc2", b"\xec\x8b\x9c"]
+    for _ in range(5000):
+        s = b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 10)))
+        assert wrs.utf8_lossy(s) == s.decode("utf-8", "replace").encode(), s
+    # a character split across two segments: each half is replaced separately (not re-joined)
+    full = "감사".encode()
+    assert wrs.utf8_lossy(full[:2]) + wrs.utf8_lossy(full[2:]) == "\ufffd\ufffd사".encode()
