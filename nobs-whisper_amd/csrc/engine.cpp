@@ -131,9 +131,10 @@ static void free_ws(Workspace& w) {
     // are freed with their parent
     void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
                   w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk,
-                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs};
+                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs, w.qtiles};
     for (void* p : ps) dfree(p);
     if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
+    if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
     if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
     if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
     w = Workspace();
@@ -196,8 +197,9 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         for (void* p : {w.cross, w.self, (void*)w.dx, w.dh, w.dq, w.datt, w.dff, w.lrow, (void*)w.logits, (void*)w.probs,
                         (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs, (void*)w.splitk, w.enc, w.qx,
-                        (void*)w.xo, (void*)w.xml, (void*)w.kvslot})
+                        (void*)w.xo, (void*)w.xml, (void*)w.kvslot, (void*)w.qtiles})
             dfree(p);
+        if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
         w.cross = w.enc = w.qx = nullptr;
         w.xo = w.xml = nullptr;
         w.splitk_elems = 16L * std::min(n_tok, 256) * 4 * (long)d;
@@ -248,6 +250,8 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         w.n_len = w.n_samp + n_jobs;
         w.mel_max = w.n_len + n_jobs;
         WM_CHECK(hipHostMalloc((void**)&w.h_ints, ((size_t)5 * n_tok + n_jobs) * sizeof(int) + 64, 0));
+        WM_CHECK(hipMalloc((void**)&w.qtiles, (size_t)n_tok * sizeof(int2)));
+        WM_CHECK(hipHostMalloc((void**)&w.h_qtiles, (size_t)n_tok * sizeof(int2), 0));
         WM_CHECK(hipHostMalloc((void**)&w.h_tout, (size_t)n_jobs * sizeof(TokOut), 0));
         WM_CHECK(hipHostMalloc((void**)&w.h_ctl, (size_t)n_jobs * sizeof(SeqCtl), 0));
         w.cap_jobs = n_jobs;
@@ -452,7 +456,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
 // Token metadata must already be in w.h_ints: [tok | pos | slot | - | - ] with stride cap_tok and
 // lrows at 5*cap_tok.
 // token metadata (already in w.h_ints: [tok | pos | slot | - | -], lrows at 5*cap_tok) -> device
-static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) {
+static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, bool tiles) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
     int* hi = w.h_ints;
@@ -465,6 +469,17 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows) 
     }
     s->cur_self_work = self_kv * hp.n_text_head * 64 * 2 * 2;
     WM_CHECK(hipMemcpyAsync(w.tok, hi, ((size_t)5 * ct + n_rows) * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    if (!tiles) return;
+    // prefill attention tiles: runs of <= 64 consecutive tokens of one slot with increasing positions
+    int nt = 0;
+    for (int i = 0; i < n_tok; i++) {
+        const bool cont = i > 0 && hi[2 * ct + i] == hi[2 * ct + i - 1] && hi[ct + i] > hi[ct + i - 1] &&
+                          w.h_qtiles[nt - 1].y < 64;
+        if (cont) w.h_qtiles[nt - 1].y++;
+        else w.h_qtiles[nt++] = make_int2(i, 1);
+    }
+    w.n_qtiles = nt;
+    WM_CHECK(hipMemcpyAsync(w.qtiles, w.h_qtiles, (size_t)nt * sizeof(int2), hipMemcpyHostToDevice, s->stream));
 }
 
 // One group of decoder rows on one stream: rows [r0, r0+n) of the token arrays and activations,
@@ -541,7 +556,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             g.ctx = hp.n_text_ctx; g.d = d;
             gemm(KCLS, EPI_QKV_DEC, g);
             KT kt(s, K_ATTN_SELF, self_share, st);
-            launch_attn_decode(dt, dq, d, w.self, slot, nkv_self, n_tok, L, l, H, hp.n_text_ctx, d, datt, 0, st);
+            launch_attn_prefill(dt, dq, d, w.self, slot, nkv_self, w.qtiles, w.n_qtiles, L, l, H, hp.n_text_ctx, d, datt, st);
         }
         resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
         if (xdirect) {
@@ -574,7 +589,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
             gemm(KCLS, EPI_STORE, g);
             KT kt(s, K_OTHER, (double)n_tok * hp.n_audio_ctx * kvrow, st);
-            launch_attn_decode(dt, dq, d, w.cross, slot, nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, datt, 2, st);
+            launch_attn_prefill(dt, dq, d, w.cross, slot, nkv_cross, w.qtiles, w.n_qtiles, L, l, H, hp.n_audio_ctx, d, datt, st);
         }
         resid(datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
         gemm(KCLS, EPI_GELU, gemm_plain(dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d));
@@ -636,14 +651,22 @@ static void ensure_cross_cache(Context* c, whisper_state* s, const std::vector<i
     const int d = hp.n_audio_state, T = hp.n_audio_ctx, L = hp.n_text_layer;
     const size_t E = esize(c->dt);
     if (!w.cross) WM_CHECK(hipMalloc(&w.cross, (size_t)w.cap_jobs * L * 2 * T * d * E));
-    for (int sl : slots) {
-        if (w.cross_fresh[sl]) continue;
-        GemmArgs g = gemm_plain((const char*)w.enc + (size_t)sl * T * d * E, T, d, c->w.wkv_cross, 2 * L * d, c->w.bkv_cross,
-                                nullptr, 0);
+    std::vector<int> stale;
+    for (int sl : slots)
+        if (!w.cross_fresh[sl]) stale.push_back(sl);
+    std::sort(stale.begin(), stale.end());
+    // one GEMM per run of consecutive slots (E is slot-major, so a run is one [k*T][d] matrix)
+    for (size_t a = 0; a < stale.size();) {
+        size_t b = a + 1;
+        while (b < stale.size() && stale[b] == stale[b - 1] + 1) b++;
+        const int sl = stale[a], k = (int)(b - a);
+        GemmArgs g = gemm_plain((const char*)w.enc + (size_t)sl * T * d * E, k * T, d, c->w.wkv_cross, 2 * L * d,
+                                c->w.bkv_cross, nullptr, 0);
         g.scale = c->k_scale;
         g.cache = w.cross; g.row_slot = w.kvslot + sl; g.L = L; g.H = hp.n_text_head; g.ctx = T; g.d = d;
         tgemm(s, K_GEMM_ENC, c->dt, EPI_CROSSKV, g, s->stream);
-        w.cross_fresh[sl] = 1;
+        for (size_t i = a; i < b; i++) w.cross_fresh[stale[i]] = 1;
+        a = b;
     }
 }
 
@@ -665,7 +688,7 @@ static bool choose_xdirect(Context* c, whisper_state* s, int n_tok) {
 
 static void decoder_forward(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity = false) {
     const bool xdirect = choose_xdirect(c, s, n_tok);
-    decoder_upload(c, s, n_tok, n_rows);
+    decoder_upload(c, s, n_tok, n_rows, true);
     decoder_launch(c, s, n_tok, n_rows, rows_identity, xdirect);
 }
 
@@ -965,7 +988,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     Context* c = S.c;
     whisper_state* s = S.s;
     const int n = (int)act.size();
-    decoder_upload(c, s, n, n);
+    decoder_upload(c, s, n, n, false);
     const bool any = logits_prepare(S, act, false);
     if (!use_graphs()) {
         decoder_launch(c, s, n, n, true, c->cross_direct);

@@ -141,6 +141,9 @@ struct Workspace {
     int *n_samp = nullptr, *n_len = nullptr, *mel_max = nullptr;
     // host pinned staging
     int* h_ints = nullptr;
+    int2* qtiles = nullptr;   // prefill attention tiles {first token, count} (cap_tok), device
+    int2* h_qtiles = nullptr; // the same, pinned host staging
+    int n_qtiles = 0;
     TokOut* h_tout = nullptr;
     SeqCtl* h_ctl = nullptr;
 };

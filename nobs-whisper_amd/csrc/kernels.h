@@ -76,6 +76,12 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
                         int n, int L, int layer, int H, int ctx, int d, void* out, int kind, hipStream_t st);
 
+// Prefill: the same attention for runs of consecutive tokens of one clip, tiles[t] = {first token,
+// count <= 64} (int2), one workgroup per (tile, head); K/V staged once per tile.
+void launch_attn_prefill(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
+                         const void* tiles, int n_tiles, int L, int layer, int H, int ctx, int d, void* out,
+                         hipStream_t st);
+
 // Decode-step attention with the projection GEMM's split-K reduce fused into its prologue.
 // Slab z holds rows [M][ld] of partial sums; the value of (row i, column c) is
 // sum_z ws[z*zstride + i*ld + c] + bias[c] (the same order as the standalone reduce).

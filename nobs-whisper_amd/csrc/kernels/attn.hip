@@ -601,6 +601,169 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Prefill attention (prompts: the app's vocabulary prompt is ~170 tokens per clip, whisper.rs:98-109,
+// config.rs:40-42): one workgroup = up to 64 consecutive query tokens of ONE clip (a host-built tile
+// list) x one head, 4 waves x 16 query rows, over that clip's cache rows [0, n_kv[i]) (the self cache
+// with n_kv = pos + 1, causal, or the cross cache, 1500 rows). Each K/V tile is staged once in LDS for
+// all 64 queries (the one-query-per-workgroup kernel above re-reads the clip's whole cache per token).
+// Two passes keep ggml's soft_max order (normalise, then round P to the f16 src1 of P.V): pass 1
+// S = Q.K^T by MFMA with an online row max and sum; pass 2 S again, P = (T)(exp(S - max) / sum),
+// O += P.V by MFMA (K tiles row-major and V tiles transposed in XOR-swizzled LDS images, as
+// attn_enc_kernel). Rows of a tile must have non-decreasing n_kv (positions increase).
+template <typename T>
+__global__ void __launch_bounds__(256) attn_prefill_kernel(const T* __restrict__ q, int q_stride, const T* __restrict__ cache,
+                                                           const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
+                                                           const int2* __restrict__ tiles, int L, int layer, int H,
+                                                           int ctx, int d, T* __restrict__ out) {
+    typedef typename Frag<T>::type FT;
+    const int2 tl = tiles[blockIdx.x];
+    const int i0 = tl.x, cnt = tl.y, h = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long s = slot[i0];
+    const T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
+    const T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
+    __shared__ u32x4 Ks[64 * 8];
+    __shared__ u32x4 Vts[64 * 8];
+    __shared__ u32x4 Ps[4][16 * 8];
+    const u32x4 zero = {0, 0, 0, 0};
+    const int kv_end = n_kv_arr[i0 + cnt - 1];
+    FT qf[2];
+    {
+        const int row = wave * 16 + (lane & 15);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+            const int ch = s2 * 4 + (lane >> 4);
+            const u32x4 v = row < cnt ? *(const u32x4*)(q + (long)(i0 + row) * q_stride + h * 64 + ch * 8) : zero;
+            qf[s2] = __builtin_bit_cast(FT, v);
+        }
+    }
+    int nkv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int row = wave * 16 + (lane >> 4) * 4 + r;
+        nkv[r] = row < cnt ? n_kv_arr[i0 + row] : 0;
+    }
+    const int n_kt = (kv_end + 63) / 64;
+    auto stage_k = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int c = tid + i * 256, key = c >> 3, kc = c & 7, kg = kt * 64 + key;
+            Ks[key * 8 + swz(key, kc)] = kg < kv_end ? *(const u32x4*)(K + (long)kg * 64 + kc * 8) : zero;
+        }
+    };
+    auto scores = [&](int kt, f32x4 (&sacc)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            sacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int row = j * 16 + (lane & 15);
+                const FT kf = __builtin_bit_cast(FT, Ks[row * 8 + swz(row, s2 * 4 + (lane >> 4))]);
+                sacc[j] = mfma16x16x32(qf[s2], kf, sacc[j]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int key = kt * 64 + j * 16 + (lane & 15);
+                if (key >= nkv[r]) sacc[j][r] = -INFINITY;
+            }
+        }
+    };
+    // pass 1: row max and sum (online)
+    float m_i[4], l_i[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) { m_i[r] = -INFINITY; l_i[r] = 0.0f; }
+    for (int kt = 0; kt < n_kt; kt++) {
+        __syncthreads();
+        stage_k(kt);
+        __syncthreads();
+        f32x4 sacc[4];
+        scores(kt, sacc);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float mx = fmaxf(fmaxf(sacc[0][r], sacc[1][r]), fmaxf(sacc[2][r], sacc[3][r]));
+            for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2));
+            const float mn = fmaxf(m_i[r], mx);
+            float sum = 0.0f;
+            if (mn != -INFINITY) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) sum += expf(sacc[j][r] - mn);
+            }
+            for (int o2 = 1; o2 < 16; o2 <<= 1) sum += __shfl_xor(sum, o2);
+            l_i[r] = (m_i[r] == -INFINITY ? 0.0f : l_i[r] * expf(m_i[r] - mn)) + sum;
+            m_i[r] = mn;
+        }
+    }
+    float inv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) inv[r] = l_i[r] > 0.0f ? 1.0f / l_i[r] : 0.0f;
+    // pass 2: P = (T)(exp(S - max) * (1 / sum)), O += P.V
+    f32x4 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    T* Vt_el = (T*)Vts;
+    T* P_el = (T*)Ps[wave];
+    for (int kt = 0; kt < n_kt; kt++) {
+        __syncthreads();
+        stage_k(kt);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int c = tid + i * 256, key = c >> 3, kc = c & 7, kg = kt * 64 + key;
+            const u32x4 vv = kg < kv_end ? *(const u32x4*)(V + (long)kg * 64 + kc * 8) : zero;
+            const T* ve = (const T*)&vv;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int dim = kc * 8 + e;
+                Vt_el[(dim * 8 + swz(dim, key >> 3)) * 8 + (key & 7)] = ve[e];
+            }
+        }
+        __syncthreads();
+        f32x4 sacc[4];
+        scores(kt, sacc);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float p = sacc[j][r] == -INFINITY ? 0.0f : expf(sacc[j][r] - m_i[r]) * inv[r];
+                const int row = (lane >> 4) * 4 + r, key = j * 16 + (lane & 15);
+                P_el[(row * 8 + swz(row, key >> 3)) * 8 + (key & 7)] = (T)p;
+            }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P stores landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+            const int prow = lane & 15;
+            const FT pf = __builtin_bit_cast(FT, Ps[wave][prow * 8 + swz(prow, s2 * 4 + (lane >> 4))]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int vrow = j * 16 + (lane & 15);
+                const FT vf = __builtin_bit_cast(FT, Vts[vrow * 8 + swz(vrow, s2 * 4 + (lane >> 4))]);
+                o[j] = mfma16x16x32(pf, vf, o[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int row = wave * 16 + (lane >> 4) * 4 + r;
+        if (row >= cnt) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[(long)(i0 + row) * d + h * 64 + j * 16 + (lane & 15)] = (T)o[j][r];
+    }
+}
+
+void launch_attn_prefill(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,
+                         const void* tiles, int n_tiles, int L, int layer, int H, int ctx, int d, void* out,
+                         hipStream_t st) {
+    if (n_tiles <= 0) return;
+    dim3 grid(n_tiles, H);
+    if (dt == DType::F16)
+        attn_prefill_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, q_stride, (const half_t*)cache, slot, n_kv,
+                                                          (const int2*)tiles, L, layer, H, ctx, d, (half_t*)out);
+    else
+        attn_prefill_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, q_stride, (const bf16_t*)cache, slot, n_kv,
+                                                          (const int2*)tiles, L, layer, H, ctx, d, (bf16_t*)out);
+}
+
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st) {
     static const int variant = [] {
         const char* e = getenv("WHISPER_MI355X_ATTN");
