@@ -160,6 +160,26 @@ static const int kXDirectMaxTok = 8;
 // lazy-rescale threshold of the direct cross attention's online softmax (log2 units: P <= 2^8)
 static const float kXattnThr = 8.0f;
 
+// Cross attention form per call. The direct form reads E once per clip and layer (half the bytes of
+// the cached K + V) but its split partials are [H][d] per (clip, split) whatever the batch, and it
+// adds two launches per layer (Q' projection, combine); at a few clips a step is launch- and
+// latency-bound and the cached form (one attention kernel, whisper.cpp's own numerics) wins: the
+// cross K/V of a window then costs one GEMM at encode time. WHISPER_MI355X_CROSS=direct|cache
+// forces a form; otherwise direct above WHISPER_MI355X_CROSS_CACHE_MAX (default 32) clips.
+static bool pick_direct(Context* c, int n_jobs) {
+    if (!c->cross_direct) return false;
+    static const int mode = [] {
+        const char* e = getenv("WHISPER_MI355X_CROSS");
+        return !e ? 0 : strcmp(e, "direct") == 0 ? 1 : strcmp(e, "cache") == 0 ? 2 : 0;
+    }();
+    static const int cache_max = [] {
+        const char* e = getenv("WHISPER_MI355X_CROSS_CACHE_MAX");
+        return e ? atoi(e) : 32;
+    }();
+    if (mode) return mode == 1;
+    return n_jobs > cache_max;
+}
+
 static int enc_batch_cap() {
     const char* e = getenv("WHISPER_MI355X_ENC_BATCH");
     int v = e ? atoi(e) : 32;
@@ -202,24 +222,12 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
         w.cross = w.enc = w.qx = nullptr;
         w.xo = w.xml = nullptr;
+        w.cap_xq = 0;
         w.splitk_elems = 16L * std::min(n_tok, 256) * 4 * (long)d;
         WM_CHECK(hipMalloc((void**)&w.splitk, w.splitk_elems * 4));
         if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
         if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
         if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
-        if (c->cross_direct) {
-            // no cross K/V cache up front: decode steps (and short prefills) read E directly
-            const int H = hp.n_text_head;
-            w.cap_xq = std::max(kXDirectMaxTok * n_jobs, 128);
-            // n * xattn_splits(n) <= max(n, 255 + n); two decode row groups at most double that
-            const size_t xo_rows = (size_t)std::max(w.cap_xq, 512) + n_jobs + 512;
-            WM_CHECK(hipMalloc(&w.enc, (size_t)n_jobs * T * d * E));
-            WM_CHECK(hipMalloc(&w.qx, (size_t)w.cap_xq * 2 * H * d * E));
-            WM_CHECK(hipMalloc((void**)&w.xo, xo_rows * H * d * 4));
-            WM_CHECK(hipMalloc((void**)&w.xml, xo_rows * H * 2 * 4));
-        } else {
-            WM_CHECK(hipMalloc(&w.cross, (size_t)n_jobs * L * 2 * T * d * E));
-        }
         w.cross_fresh.assign(n_jobs, 0);
         {
             std::vector<int> ident(n_jobs);
@@ -258,6 +266,20 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         w.cap_tok = n_tok;
     }
     (void)unused;
+    // the buffers of this call's cross attention form (allocated on first use, kept)
+    if (s->direct && !w.enc) {
+        // no cross K/V cache up front: decode steps (and short prefills) read E directly
+        const int H = hp.n_text_head;
+        w.cap_xq = std::max(kXDirectMaxTok * w.cap_jobs, 128);
+        // n * xattn_splits(n) <= max(n, 255 + n); two decode row groups at most double that
+        const size_t xo_rows = (size_t)std::max(w.cap_xq, 512) + w.cap_jobs + 512;
+        WM_CHECK(hipMalloc(&w.enc, (size_t)w.cap_jobs * T * d * E));
+        WM_CHECK(hipMalloc(&w.qx, (size_t)w.cap_xq * 2 * H * d * E));
+        WM_CHECK(hipMalloc((void**)&w.xo, xo_rows * H * d * 4));
+        WM_CHECK(hipMalloc((void**)&w.xml, xo_rows * H * 2 * 4));
+    }
+    if (!s->direct && !w.cross)
+        WM_CHECK(hipMalloc(&w.cross, (size_t)w.cap_jobs * hp.n_text_layer * 2 * T * d * E));
 }
 
 // ---- mel ------------------------------------------------------------------------------------------
@@ -265,6 +287,7 @@ static inline int mel_n_len(int n) { return (n + 16000 * 30) / 160; }
 static inline int mel_n_len_org(int n) { return 1 + (int)(((int64_t)n + 200 - 400) / 160); }
 
 int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int* n, int n_jobs, bool on_device) {
+    s->direct = pick_direct(c, n_jobs);
     ensure_ws(c, s, n_jobs);
     Workspace& w = s->ws;
     const int nm = c->hp.n_mels;
@@ -431,7 +454,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
             tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, L.w2, d, L.b2, w.x, d), st);
         }
         launch_layernorm(dt, w.x, nullptr, M, d, W.lnpost_w, W.lnpost_b, w.hn, st);
-        if (c->cross_direct) {
+        if (s->direct) {
             // keep E per slot for the direct cross attention; the slot's cross K/V (if any) is stale
             for (int k = 0; k < nb; k++) {
                 WM_CHECK(hipMemcpyAsync((char*)w.enc + (size_t)slots[b0 + k] * T * d * E, (const char*)w.hn + (size_t)k * T * d * E,
@@ -444,6 +467,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
             g.scale = c->k_scale;
             g.cache = w.cross; g.row_slot = d_slot; g.L = hp.n_text_layer; g.H = hp.n_text_head; g.ctx = T; g.d = d;
             tgemm(s, KCLS, dt, EPI_CROSSKV, g, st);
+            for (int k = 0; k < nb; k++) w.cross_fresh[slots[b0 + k]] = 1;
         }
         WM_CHECK(hipStreamSynchronize(st));  // h_ints reused by the next micro-batch
     }
@@ -673,7 +697,7 @@ static void ensure_cross_cache(Context* c, whisper_state* s, const std::vector<i
 // Direct cross attention for this forward (tokens/slots already in w.h_ints)? Yes for one-token
 // steps and short prompts; otherwise the clips involved get a cross K/V cache first.
 static bool choose_xdirect(Context* c, whisper_state* s, int n_tok) {
-    if (!c->cross_direct) return false;
+    if (!s->direct) return false;
     Workspace& w = s->ws;
     const int* slot = w.h_ints + 2 * w.cap_tok;
     std::vector<int> cnt(w.cap_jobs, 0);
@@ -991,20 +1015,20 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     decoder_upload(c, s, n, n, false);
     const bool any = logits_prepare(S, act, false);
     if (!use_graphs()) {
-        decoder_launch(c, s, n, n, true, c->cross_direct);
+        decoder_launch(c, s, n, n, true, s->direct);
         logits_launch(c, s, n);
         logits_finish(S, n, any, probs_rows);
         return;
     }
     whisper_state::DecGraph* G = nullptr;
     for (auto& g : s->dec_graphs)
-        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask) G = &g;
+        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct) G = &g;
     if (!G) {
-        whisper_state::DecGraph g{n, n, s->ktime_mask, nullptr, {}};
+        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, nullptr, {}};
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        decoder_launch(c, s, n, n, true, c->cross_direct);
+        decoder_launch(c, s, n, n, true, s->direct);
         logits_launch(c, s, n);
         WM_CHECK(hipStreamEndCapture(s->stream, &graph));
         s->capture_ev = nullptr;
@@ -1041,6 +1065,7 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
     s->decisions.assign(n_jobs, {});
     s->decoded_tokens = 0;
     double t0 = now_ms();
+    s->direct = pick_direct(c, n_jobs);
     ensure_ws(c, s, n_jobs);
     compute_mel(c, s, pcm, n, n_jobs, on_device);
     S.t_mel = now_ms() - t0;

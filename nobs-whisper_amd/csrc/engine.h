@@ -77,8 +77,8 @@ struct Context {
     std::mutex timings_mu;  // states on different threads add their phase times here
     whisper_state* default_state = nullptr;  // whisper_init_from_file_with_params (with state)
     float k_scale = 0.0f;                    // d_head^-0.25
-    // Cross attention straight from the encoder output (kernels/xattn.hip) instead of through a
-    // materialised cross K/V cache; set at load (WHISPER_MI355X_CROSS=cache turns it off).
+    // Cross attention straight from the encoder output (kernels/xattn.hip) is available for this
+    // model (its per-head transposed Wk is in the arena); each call picks direct or cached form.
     bool cross_direct = false;
     std::string model_type;
     whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
@@ -164,6 +164,9 @@ struct whisper_state {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     wm::Workspace ws;
+    // cross attention form of the current call: straight from the encoder output (large batches) or
+    // through a per-clip cross K/V cache (small batches, and whisper.cpp's own form)
+    bool direct = false;
     // whisper.h single-clip results (job 0 of the last call) + batch results
     std::vector<std::vector<wm::Segment>> results;
     std::vector<int> lang_ids;
@@ -184,7 +187,7 @@ struct whisper_state {
     std::vector<KPending> kpending;
     std::vector<hipEvent_t> kpool;
     // decode steps replayed as hipGraphs (one per active-sequence count and timing mask)
-    struct DecGraph { int n_tok, n_rows, mask; hipGraphExec_t exec; std::vector<KPending> ev; };
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step

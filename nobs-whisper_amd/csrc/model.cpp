@@ -319,10 +319,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     if (!ok) { munmap(map, fsize); return false; }
     mat(&W.wkv_cross, xkv, (long)2 * Ld * d, d, xrows, false, 0);
     vecf(&W.bkv_cross, xkvb, xbn);
-    {
-        const char* e = getenv("WHISPER_MI355X_CROSS");
-        c->cross_direct = xattn_supported(d) && hp.n_text_head * 64 == d && !(e && strcmp(e, "cache") == 0);
-    }
+    c->cross_direct = xattn_supported(d) && hp.n_text_head * 64 == d;
     if (c->cross_direct) {
         // cross K weights per head, transposed: wkT[l][h][c][j] = Wk_l[h*64 + j][c], the B operand of
         // the Q' projection Q'_h = s * Wk_h^T q_h (kernels/xattn.hip)
