@@ -551,9 +551,9 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         gemm(KCLS, EPI_RESID, g);
         if (!fused && lnw) launch_layernorm(dt, dx, nullptr, n_tok, d, lnw, lnb, dh, st);
     };
-    if (fused) launch_embed_ln(dt, W.tok_emb, W.pos_d, tok, pos, n_tok, d, dx, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
+    if (fused) launch_embed_ln(dt, W.tok_emb_f32 ? (const void*)W.tok_emb_f32 : W.tok_emb, W.tok_emb_f32 != nullptr, W.pos_d, tok, pos, n_tok, d, dx, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
     else {
-        launch_embed(dt, W.tok_emb, W.pos_d, tok, pos, n_tok, d, dx, st);
+        launch_embed(dt, W.tok_emb_f32 ? (const void*)W.tok_emb_f32 : W.tok_emb, W.tok_emb_f32 != nullptr, W.pos_d, tok, pos, n_tok, d, dx, st);
         launch_layernorm(dt, dx, nullptr, n_tok, d, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
     }
     // decode steps: the QKV (and, cache mode, cross-Q) projections leave split-K partial sums that

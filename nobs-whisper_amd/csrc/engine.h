@@ -53,6 +53,7 @@ struct Weights {
     float* pos_e;
     float *lnpost_w, *lnpost_b;
     void* tok_emb; float* pos_d;
+    float* tok_emb_f32 = nullptr;       // quantized GGML embedding: exact f32 rows for the lookups
     float *lnd_w, *lnd_b;
     void* wkv_cross; float* bkv_cross;  // [L_d][2][d][d], bias [L_d][2][d] (K part zero)
     void* wkT = nullptr;                // [L_d][H][d][64]: cross K per head, transposed (direct cross attention)

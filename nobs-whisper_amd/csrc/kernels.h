@@ -16,12 +16,13 @@ void launch_mel_normalize(const float* d_mel, int nl, int n_samples, const int* 
 // y[i] = LN(x[row(i)]) * w + b, x f32 [.][D] (row stride D), y T [M][D]; row(i) = rows ? rows[i] : i
 void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b,
                       void* y, hipStream_t st);
-// x[i][:] = tok_emb[tok[i]][:] + pos_emb[pos[i]][:]   (f32 out)
-void launch_embed(DType dt, const void* tok_emb, const float* pos_emb, const int* tok, const int* pos, int n, int D,
-                  float* x, hipStream_t st);
+// x[i][:] = tok_emb[tok[i]][:] + pos_emb[pos[i]][:]   (f32 out; tok_emb in the MFMA type, or f32
+// when te_f32: a quantized GGML embedding's exact dequantized rows)
+void launch_embed(DType dt, const void* tok_emb, bool te_f32, const float* pos_emb, const int* tok, const int* pos,
+                  int n, int D, float* x, hipStream_t st);
 // embedding fused with the first LayerNorm: x as above, y[i] = LN(x[i]) * w + b (T out)
-void launch_embed_ln(DType dt, const void* tok_emb, const float* pos_emb, const int* tok, const int* pos, int n, int D,
-                     float* x, const float* w, const float* b, void* y, hipStream_t st);
+void launch_embed_ln(DType dt, const void* tok_emb, bool te_f32, const float* pos_emb, const int* tok, const int* pos,
+                     int n, int D, float* x, const float* w, const float* b, void* y, hipStream_t st);
 
 // ---- GEMM (kernels/gemm.hip): C[M][N] = A[M][K] . B[N][K]^T + bias, fused epilogues --------------
 enum Epi : int {

@@ -181,8 +181,10 @@ void launch_layernorm_fp8(const float* x, int M, int D, const float* w, const fl
     abort();
 }
 
-template <typename T>
-__global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__ pe, const int* __restrict__ tok,
+// TE: the token-embedding table's type: the MFMA type, or f32 for a quantized GGML embedding that
+// ggml_get_rows dequantizes to f32 (exact q*d (+m)) while the logits matmul sees it rounded to f16
+template <typename TE>
+__global__ void embed_kernel(const TE* __restrict__ te, const float* __restrict__ pe, const int* __restrict__ tok,
                              const int* __restrict__ pos, int D, float* __restrict__ x) {
     const int i = blockIdx.x;
     const long t = tok[i], p = pos[i];
@@ -190,8 +192,8 @@ __global__ void embed_kernel(const T* __restrict__ te, const float* __restrict__
 }
 
 // decoder token + position embedding fused with the first layer's LayerNorm (one block per token)
-template <typename T, int NPT>
-__global__ void __launch_bounds__(256) embed_ln_kernel(const T* __restrict__ te, const float* __restrict__ pe,
+template <typename T, int NPT, typename TE>
+__global__ void __launch_bounds__(256) embed_ln_kernel(const TE* __restrict__ te, const float* __restrict__ pe,
                                                        const int* __restrict__ tok, const int* __restrict__ pos, int D,
                                                        float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ b, T* __restrict__ y) {
@@ -211,17 +213,19 @@ __global__ void __launch_bounds__(256) embed_ln_kernel(const T* __restrict__ te,
     block256_layernorm<T, NPT>(v, D, w, b, y + (long)i * D, sh);
 }
 
-void launch_embed_ln(DType dt, const void* te, const float* pe, const int* tok, const int* pos, int n, int D, float* x,
-                     const float* w, const float* b, void* y, hipStream_t st) {
+void launch_embed_ln(DType dt, const void* te, bool te_f32, const float* pe, const int* tok, const int* pos, int n, int D,
+                     float* x, const float* w, const float* b, void* y, hipStream_t st) {
     if (n <= 0) return;
     if (D > 2048) { fprintf(stderr, "whisper_mi355x: embed LN width %d > 2048\n", D); abort(); }
+#define WM_ELN(T, NPT)                                                                                                    \
+    if (te_f32) embed_ln_kernel<T, NPT, float><<<n, 256, 0, st>>>((const float*)te, pe, tok, pos, D, x, w, b, (T*)y);       \
+    else embed_ln_kernel<T, NPT, T><<<n, 256, 0, st>>>((const T*)te, pe, tok, pos, D, x, w, b, (T*)y)
     if (D <= 1024) {
-        if (dt == DType::F16) embed_ln_kernel<half_t, 4><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x, w, b, (half_t*)y);
-        else embed_ln_kernel<bf16_t, 4><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x, w, b, (bf16_t*)y);
+        if (dt == DType::F16) { WM_ELN(half_t, 4); } else { WM_ELN(bf16_t, 4); }
     } else {
-        if (dt == DType::F16) embed_ln_kernel<half_t, 8><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x, w, b, (half_t*)y);
-        else embed_ln_kernel<bf16_t, 8><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x, w, b, (bf16_t*)y);
+        if (dt == DType::F16) { WM_ELN(half_t, 8); } else { WM_ELN(bf16_t, 8); }
     }
+#undef WM_ELN
 }
 
 void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, const float* w, const float* b, void* y,
@@ -240,10 +244,11 @@ void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, c
     abort();
 }
 
-void launch_embed(DType dt, const void* te, const float* pe, const int* tok, const int* pos, int n, int D, float* x,
-                  hipStream_t st) {
+void launch_embed(DType dt, const void* te, bool te_f32, const float* pe, const int* tok, const int* pos, int n, int D,
+                  float* x, hipStream_t st) {
     if (n <= 0) return;
-    if (dt == DType::F16) embed_kernel<half_t><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x);
+    if (te_f32) embed_kernel<float><<<n, 256, 0, st>>>((const float*)te, pe, tok, pos, D, x);
+    else if (dt == DType::F16) embed_kernel<half_t><<<n, 256, 0, st>>>((const half_t*)te, pe, tok, pos, D, x);
     else embed_kernel<bf16_t><<<n, 256, 0, st>>>((const bf16_t*)te, pe, tok, pos, D, x);
 }
 

@@ -50,11 +50,41 @@ int lang_index(const char* code) {
 namespace {
 
 struct TensorRef {
-    int type;  // 0 f32, 1 f16
+    int type;  // 0 f32, 1 f16, or a GGML block-quantized type (2 q4_0, 3 q4_1, 6 q5_0, 7 q5_1, 8 q8_0)
     std::vector<int> ne;
     const char* data;
     size_t nel;
 };
+
+// GGML block quantization [ext, ggml-common.h / ggml-quants.c dequantize_row_*]: blocks of 32 weights,
+// y = q * d (q5_0: q - 16, q4_0: q - 8, q8_0: signed bytes) or q * d + m (q5_1, q4_1); q * d is exact
+// in f32 (<= 8-bit q times an f16 d). The app's catalog ships q5_1 and q5_0 files (model.rs:153-186).
+int block_bytes(int type) {
+    switch (type) {
+        case 2: return 18; case 3: return 20; case 6: return 22; case 7: return 24; case 8: return 34;
+        default: return 0;
+    }
+}
+float hf(const uint8_t* p) { uint16_t h; memcpy(&h, p, 2); return h2f(h); }
+void dequant_block(int type, const uint8_t* b, float* y) {
+    if (type == 8) {
+        const float d = hf(b);
+        for (int j = 0; j < 32; j++) y[j] = (float)(int8_t)b[2 + j] * d;
+        return;
+    }
+    const bool has_m = type == 3 || type == 7, has_h = type == 6 || type == 7;
+    const float d = hf(b), m = has_m ? hf(b + 2) : 0.0f;
+    const uint8_t* p = b + (has_m ? 4 : 2);
+    uint32_t qh = 0;
+    if (has_h) { memcpy(&qh, p, 4); p += 4; }
+    const int off = has_m ? 0 : (has_h ? 16 : 8);
+    for (int j = 0; j < 16; j++) {
+        int x0 = p[j] & 0x0F, x1 = p[j] >> 4;
+        if (has_h) { x0 |= ((qh >> j) << 4) & 0x10; x1 |= (qh >> (j + 12)) & 0x10; }
+        y[j] = has_m ? (float)x0 * d + m : (float)(x0 - off) * d;
+        y[j + 16] = has_m ? (float)x1 * d + m : (float)(x1 - off) * d;
+    }
+}
 
 struct Reader {
     const char* p;
@@ -87,8 +117,19 @@ struct Arena {
 
 float elem(const TensorRef& t, size_t i) {
     if (t.type == 0) { float f; memcpy(&f, t.data + 4 * i, 4); return f; }
-    uint16_t h; memcpy(&h, t.data + 2 * i, 2);
-    return h2f(h);
+    if (t.type == 1) { uint16_t h; memcpy(&h, t.data + 2 * i, 2); return h2f(h); }
+    float y[32];
+    dequant_block(t.type, (const uint8_t*)t.data + (i / 32) * block_bytes(t.type), y);
+    return y[i % 32];
+}
+// row r (cols values) of a 2-D tensor as f32
+void row_f32(const TensorRef& t, long r, long cols, float* out) {
+    if (t.type == 0 || t.type == 1) {
+        for (long k = 0; k < cols; k++) out[k] = elem(t, r * cols + k);
+        return;
+    }
+    const uint8_t* b = (const uint8_t*)t.data + (r * cols / 32) * block_bytes(t.type);
+    for (long k = 0; k < cols; k += 32) dequant_block(t.type, b + (k / 32) * block_bytes(t.type), out + k);
 }
 
 }  // namespace
@@ -150,6 +191,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     c->dt = dt;
     c->device = device;
     c->hp = r.get<Hparams>();
+    c->hp.ftype %= 1000;  // GGML_QNT_VERSION * GGML_QNT_VERSION_FACTOR rides on a quantized file's ftype
     const Hparams& hp = c->hp;
     if (hp.n_audio_state != hp.n_text_state || hp.n_audio_state % 64 || hp.n_audio_state / hp.n_audio_head != 64 ||
         hp.n_text_state / hp.n_text_head != 64 || hp.n_mels % 8) {
@@ -171,8 +213,11 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         for (int i = 0; i < n_dims; i++) { t.ne.push_back(r.get<int32_t>()); t.nel *= t.ne.back(); }
         const char* nm = r.take(name_len);
         if (!nm) break;
-        if (ttype != 0 && ttype != 1) { return fail("quantized tensor types are not supported yet"); }
-        t.data = r.take(t.nel * (ttype == 0 ? 4 : 2));
+        size_t bytes;
+        if (ttype == 0 || ttype == 1) bytes = t.nel * (ttype == 0 ? 4 : 2);
+        else if (block_bytes(ttype) && n_dims >= 1 && t.ne[0] % 32 == 0) bytes = t.nel / 32 * block_bytes(ttype);
+        else return fail("unsupported tensor type (f32, f16, q4_0, q4_1, q5_0, q5_1, q8_0)");
+        t.data = r.take(bytes);
         if (!t.data) break;
         tens[std::string(nm, name_len)] = t;
     }
@@ -206,9 +251,26 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         std::vector<char> b(sz);
         uint16_t* o = (uint16_t*)b.data();
         long row0 = 0;
+        std::vector<float> rowbuf(cols);
         for (size_t pi = 0; pi < parts.size(); pi++) {
             const TensorRef* t = parts[pi];
             const long nr = rows_each[pi];
+            if (t && t->type != 0 && t->type != 1) {
+                // quantized: dequantize each row (exact f32), round once to the compute type, as ggml's
+                // GPU matmuls do when they dequantize blocks into f16 tiles
+                for (long rr = 0; rr < nr; rr++) {
+                    row_f32(*t, rr, cols, rowbuf.data());
+                    for (long k = 0; k < cols; k++) {
+                        const float f = rowbuf[k];
+                        uint16_t out;
+                        if (dt == DType::F16) { _Float16 hf16 = (_Float16)f; memcpy(&out, &hf16, 2); }
+                        else out = f2bf(f);
+                        o[(row0 + rr) * cols + k] = out;
+                    }
+                }
+                row0 += nr;
+                continue;
+            }
             for (long rr = 0; rr < nr; rr++)
                 for (long k = 0; k < cols; k++) {
                     long src_k = k;
@@ -261,6 +323,14 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         vecf(&W.lnpost_w, {lpw}, {d});
         vecf(&W.lnpost_b, {lpb}, {d});
         mat(&W.tok_emb, {te}, V, d, {V}, false, 0);
+        if (te->type != 0 && te->type != 1) {
+            // ggml_get_rows dequantizes a quantized embedding to exact f32 rows (the decoder input),
+            // while the logits matmul reads the f16-rounded blocks: keep both
+            const size_t sz = (size_t)V * d * 4;
+            std::vector<char> eb(load_weights ? sz : 0);
+            for (long rr = 0; rr < V && load_weights; rr++) row_f32(*te, rr, d, (float*)eb.data() + rr * d);
+            A.add((void**)&W.tok_emb_f32, sz, std::move(eb));
+        }
         vecf(&W.pos_d, {pd}, {(long)hp.n_text_ctx * d});
         vecf(&W.lnd_w, {ldw}, {d});
         vecf(&W.lnd_b, {ldb}, {d});
@@ -327,8 +397,14 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         const size_t sz = (size_t)Ld * H * d * 64 * esz;
         std::vector<char> b(load_weights ? sz : 0);
         uint16_t* o = (uint16_t*)b.data();
+        std::vector<float> rows;
         for (int l = 0; l < Ld && load_weights; l++) {
             const TensorRef* t = xkv[2 * l];
+            const bool q = t->type != 0 && t->type != 1;
+            if (q) {
+                rows.resize((size_t)d * d);
+                for (long rr = 0; rr < d; rr++) row_f32(*t, rr, d, rows.data() + rr * d);
+            }
             for (int h = 0; h < H; h++)
                 for (int j = 0; j < 64; j++)
                     for (int k = 0; k < d; k++) {
@@ -336,7 +412,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
                         uint16_t out;
                         if (t->type == 1 && dt == DType::F16) memcpy(&out, t->data + 2 * src, 2);
                         else {
-                            const float f = elem(*t, src);
+                            const float f = q ? rows[src] : elem(*t, src);
                             if (dt == DType::F16) { _Float16 hf = (_Float16)f; memcpy(&out, &hf, 2); }
                             else out = f2bf(f);
                         }

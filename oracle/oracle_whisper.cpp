@@ -65,7 +65,29 @@ struct Vocab {
     int num_languages() const { return n_vocab - 51765 - (is_multilingual() ? 1 : 0); }
 };
 
-struct Tensor { std::vector<int> ne; std::vector<float> data; };
+struct Tensor { std::vector<int> ne; std::vector<float> data; int type = 0; };
+
+// [ext] ggml dequantize_row_q4_0/q4_1/q5_0/q5_1/q8_0: blocks of 32, y = q*d (+ m), exact in f32
+static int block_bytes(int type) {
+    switch (type) { case 2: return 18; case 3: return 20; case 6: return 22; case 7: return 24; case 8: return 34; }
+    return 0;
+}
+static void dequant_block(int type, const uint8_t* b, float* y) {
+    auto hf = [](const uint8_t* p) { uint16_t h; memcpy(&h, p, 2); return f16_to_f32(h); };
+    if (type == 8) { const float d = hf(b); for (int j = 0; j < 32; j++) y[j] = (float)(int8_t)b[2 + j] * d; return; }
+    const bool has_m = type == 3 || type == 7, has_h = type == 6 || type == 7;
+    const float d = hf(b), m = has_m ? hf(b + 2) : 0.0f;
+    const uint8_t* qs = b + (has_m ? 4 : 2);
+    uint32_t qh = 0;
+    if (has_h) { memcpy(&qh, qs, 4); qs += 4; }
+    const int off = has_m ? 0 : (has_h ? 16 : 8);
+    for (int j = 0; j < 16; j++) {
+        int x0 = qs[j] & 0x0F, x1 = qs[j] >> 4;
+        if (has_h) { x0 |= ((qh >> j) << 4) & 0x10; x1 |= (qh >> (j + 12)) & 0x10; }
+        y[j] = has_m ? (float)x0 * d + m : (float)(x0 - off) * d;
+        y[j + 16] = has_m ? (float)x1 * d + m : (float)(x1 - off) * d;
+    }
+}
 
 struct Layer {  // pointers into the tensor map
     const float *attn_ln_w, *attn_ln_b, *q_w, *q_b, *k_w, *v_w, *v_b, *o_w, *o_b;
@@ -84,6 +106,11 @@ struct Model {
     std::vector<Layer> enc, dec;
     const float *conv1_w, *conv1_b, *conv2_w, *conv2_b, *e_pe, *e_ln_w, *e_ln_b;
     const float *d_pe, *d_te, *d_ln_w, *d_ln_b;
+    // token embedding rows for the lookup: == d_te, except for a quantized embedding, whose
+    // ggml_get_rows rows are the exact f32 dequantization while its matmul (the logits) reads the
+    // blocks dequantized into f16 tiles (ggml's GPU back-ends; mode 1)
+    std::vector<float> te_lookup;
+    const float* d_te_lookup = nullptr;
 };
 
 static const float* T(Model& m, const std::string& name) {
@@ -104,6 +131,7 @@ static Model* load_model(const char* path, int mode, int n_threads) {
         uint32_t magic; rd(&magic, 4);
         if (magic != 0x67676d6c) throw 1;
         rd(&m->hp, sizeof(Hparams));
+        m->hp.ftype %= 1000;  // + 1000 * GGML_QNT_VERSION on quantized files
         rd(&m->filt_n_mel, 4); rd(&m->filt_n_fft, 4);
         m->filters.resize((size_t)m->filt_n_mel * m->filt_n_fft);
         rd(m->filters.data(), m->filters.size() * 4);
@@ -151,11 +179,16 @@ static Model* load_model(const char* path, int mode, int n_threads) {
             for (int i = 0; i < n_dims; i++) { rd(&tt.ne[i], 4); nel *= tt.ne[i]; }
             std::string name(name_len, '\0'); rd(&name[0], name_len);
             tt.data.resize(nel);
+            tt.type = ttype;
             if (ttype == 0) rd(tt.data.data(), nel * 4);
             else if (ttype == 1) {
                 std::vector<uint16_t> h(nel); rd(h.data(), nel * 2);
                 for (size_t i = 0; i < nel; i++) tt.data[i] = f16_to_f32(h[i]);
-            } else throw 2;  // quantized types: not in the oracle
+            } else if (block_bytes(ttype) && nel % 32 == 0) {
+                std::vector<uint8_t> q(nel / 32 * block_bytes(ttype));
+                rd(q.data(), q.size());
+                for (size_t blk = 0; blk < nel / 32; blk++) dequant_block(ttype, q.data() + blk * block_bytes(ttype), &tt.data[blk * 32]);
+            } else throw 2;
             m->t[name] = std::move(tt);
         }
     } catch (...) { fclose(f); delete m; return nullptr; }
@@ -167,6 +200,15 @@ static Model* load_model(const char* path, int mode, int n_threads) {
     M.e_ln_w = T(M, "encoder.ln_post.weight"); M.e_ln_b = T(M, "encoder.ln_post.bias");
     M.d_pe = T(M, "decoder.positional_embedding"); M.d_te = T(M, "decoder.token_embedding.weight");
     M.d_ln_w = T(M, "decoder.ln.weight"); M.d_ln_b = T(M, "decoder.ln.bias");
+    M.d_te_lookup = M.d_te;
+    for (auto& kv : M.t) {
+        if (kv.second.type < 2) continue;
+        if (kv.first == "decoder.token_embedding.weight") {
+            M.te_lookup = kv.second.data;
+            M.d_te_lookup = M.te_lookup.data();
+        }
+        if (M.mode) for (auto& x : kv.second.data) x = round_f16(x);  // f16 tiles of the GPU matmul
+    }
     for (int i = 0; i < M.hp.n_audio_layer; i++) {
         std::string p = "encoder.blocks." + std::to_string(i) + ".";
         Layer L{};
@@ -371,6 +413,7 @@ struct Decoder {
     bool failed = false, completed = false, has_ts = false;
     std::vector<float> probs, logits, logprobs;
     std::mt19937 rng{0};
+    float ts_gap = 1e9f;  // |timestamp logprob mass - best text logprob| of the last step (a close call too)
 };
 
 struct Segment { int64_t t0, t1; std::string text; float no_speech_prob; std::vector<TokenData> tokens; };
@@ -422,7 +465,7 @@ static void decode(Model& m, State& s, const int* tokens, int n, int n_past) {
         att((size_t)n * d), tmp((size_t)n * d), ff((size_t)n * 4 * d);
     for (int i = 0; i < n; i++)
         for (int c = 0; c < d; c++)
-            x[(size_t)i * d + c] = m.d_te[(size_t)tokens[i] * d + c] + m.d_pe[(size_t)(n_past + i) * d + c];
+            x[(size_t)i * d + c] = m.d_te_lookup[(size_t)tokens[i] * d + c] + m.d_pe[(size_t)(n_past + i) * d + c];
     auto attend = [&](const float* Q, const float* K, const float* Vv, int n_kv_of_i_base, bool causal, float* O) {
         // Q [n][d] (already scaled + rounded), K/V [n_kv][d]
 #pragma omp parallel num_threads(m.n_threads)
@@ -594,6 +637,7 @@ static void process_logits(Model& m, State& s, Decoder& dec, const OracleParams&
             if (lse > 0.0f) ts_logprob = logf(lse) + mx;
         }
         const float max_text = *std::max_element(dec.logprobs.begin(), dec.logprobs.begin() + vocab.token_beg);
+        dec.ts_gap = ts_logprob > -INFINITY && max_text > -INFINITY ? fabsf(ts_logprob - max_text) : 1e9f;
         if (ts_logprob > max_text)
             for (int i = 0; i < vocab.token_beg; ++i) { logits[i] = -INFINITY; dec.logprobs[i] = -INFINITY; }
     }
@@ -622,8 +666,9 @@ static TokenData sample_token(Model& m, State& s, Decoder& dec, bool best) {
             if (r.p < probs[i]) { second = r.p; r.id = i; r.p = probs[i]; r.plog = dec.logprobs[i]; }
             else if (second < probs[i]) second = probs[i];
         }
-        // top-2 log-probability gap of the greedy choice (how far an argmax is from flipping)
-        s.step_margin.push_back(second > 0.0f ? logf(r.p) - logf(second) : 1e9f);
+        // how far the greedy choice is from flipping: its top-2 log-probability gap, or the gap of the
+        // timestamp rule (timestamp mass vs best text token) that shaped this step's candidates
+        s.step_margin.push_back(std::min(second > 0.0f ? logf(r.p) - logf(second) : 1e9f, dec.ts_gap));
     } else {
         std::discrete_distribution<> dist(probs.begin(), probs.end());
         r.id = dist(dec.rng);
@@ -853,6 +898,17 @@ void* oracle_load(const char* path, int mode, int n_threads) {
     return load_model(path, mode, n_threads);
 }
 void oracle_free(void* m) { delete (Model*)m; }
+// a loaded tensor as the oracle computes with it (dequantized; f16-rounded in mode 1), or with
+// lookup != 0 the token-embedding rows of the decoder's lookup. Returns the element count.
+long oracle_tensor(void* mp, const char* name, int lookup, float* out, long cap) {
+    Model& m = *(Model*)mp;
+    auto it = m.t.find(name);
+    if (it == m.t.end()) return -1;
+    const long n = (long)it->second.data.size();
+    const float* src = lookup ? m.d_te_lookup : it->second.data.data();
+    if (out && cap >= n) std::copy(src, src + n, out);
+    return n;
+}
 void oracle_set_threads(void* m, int n) { ((Model*)m)->n_threads = n; }
 void* oracle_state_new(void* m) { (void)m; return new State(); }
 void oracle_state_free(void* s) { delete (State*)s; }
@@ -860,9 +916,14 @@ void oracle_state_free(void* s) { delete (State*)s; }
 int oracle_token(void* mp, const char* which) {
     Vocab& v = ((Model*)mp)->vocab;
     std::string w(which);
-    if (w == "eot") return v.token_eot; if (w == "sot") return v.token_sot; if (w == "beg") return v.token_beg;
-    if (w == "not") return v.token_not; if (w == "prev") return v.token_prev; if (w == "nosp") return v.token_nosp;
-    if (w == "solm") return v.token_solm; if (w == "transcribe") return v.token_transcribe;
+    if (w == "eot") return v.token_eot;
+    if (w == "sot") return v.token_sot;
+    if (w == "beg") return v.token_beg;
+    if (w == "not") return v.token_not;
+    if (w == "prev") return v.token_prev;
+    if (w == "nosp") return v.token_nosp;
+    if (w == "solm") return v.token_solm;
+    if (w == "transcribe") return v.token_transcribe;
     if (w == "translate") return v.token_translate;
     return -1;
 }

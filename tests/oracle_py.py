@@ -101,6 +101,7 @@ def lib():
             "oracle_step_margins": (None, [vp, fp]),
             "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
             "oracle_mel_tables": (None, [fp, fp, fp]),
+            "oracle_tensor": (C.c_long, [vp, C.c_char_p, C.c_int, fp, C.c_long]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -151,6 +152,15 @@ class Oracle:
             self.close()
         except Exception:
             pass
+
+    def tensor(self, name: str, lookup: bool = False) -> np.ndarray:
+        """A loaded tensor as the oracle computes with it (flat, ggml element order)."""
+        n = self.L.oracle_tensor(self.m, name.encode(), int(lookup), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        out = np.empty(n, np.float32)
+        self.L.oracle_tensor(self.m, name.encode(), int(lookup), _fp(out), n)
+        return out
 
     def token(self, which: str) -> int:
         return self.L.oracle_token(self.m, which.encode())
@@ -207,9 +217,11 @@ class Oracle:
         n = self.L.oracle_n_steps(self.s)
         margins = np.empty(n, np.float32)
         self.L.oracle_step_margins(self.s, _fp(margins))
+        seq = (C.c_int * 4096)()
+        n_seq = min(4096, self.L.oracle_decoder_tokens(self.s, seq, 4096))
         nd = self.L.oracle_n_decisions(self.s)
         dec = (Decision * max(1, nd))()
         self.L.oracle_decisions(self.s, C.cast(dec, C.c_void_p))
         return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
-                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins,
+                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins, seq=list(seq[:n_seq]),
                     decisions=decisions_to_dicts(dec[:nd]))

@@ -236,15 +236,133 @@ def conf_adjust(name: str, t: np.ndarray, n_vocab: int) -> np.ndarray:
     return t
 
 
-def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1) -> dict:
+# ---- GGML block quantization (the app's catalog ships small-q5_1, medium-q5_0 and large-v3-q5_0:
+# src-tauri/src/model.rs:153-186). Tensor type ids and block layouts of ggml [ext, ggml-common.h]:
+#   Q4_0 = 2: {f16 d; u8 qs[16]}            18 B / 32      Q4_1 = 3: {f16 d, m; u8 qs[16]}        20 B / 32
+#   Q5_0 = 6: {f16 d; u8 qh[4]; u8 qs[16]}   22 B / 32      Q5_1 = 7: {f16 d, m; u8 qh[4]; qs[16]} 24 B / 32
+#   Q8_0 = 8: {f16 d; i8 qs[32]}             34 B / 32
+# The file's ftype is GGML_FTYPE_MOSTLY_* + 1000 * GGML_QNT_VERSION (2). whisper.cpp's quantize tool
+# quantizes every 2-D tensor except the positional embeddings (3-D conv weights and 1-D tensors stay).
+GGML_TYPES = {"q4_0": 2, "q4_1": 3, "q5_0": 6, "q5_1": 7, "q8_0": 8}
+GGML_FTYPES = {"q4_0": 2, "q4_1": 3, "q5_0": 8, "q5_1": 9, "q8_0": 7}
+GGML_QNT_VERSION = 2
+# whisper.cpp's quantize tool: 2-D tensors only, minus these (examples/quantize, to_skip) [ext]
+QUANT_SKIP = ("encoder.conv1.bias", "encoder.conv2.bias", "encoder.positional_embedding",
+              "decoder.positional_embedding")
+BLOCK_BYTES = {2: 18, 3: 20, 6: 22, 7: 24, 8: 34}
+
+
+def read_tensors(path: str) -> dict:
+    """Parse a GGML whisper file: {name: (ggml type, ne (innermost first), raw bytes)}."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    o = 4 + 11 * 4
+    n_mel, n_fft = struct.unpack_from("<2i", buf, o)
+    o += 8 + 4 * n_mel * n_fft
+    (n_tok,) = struct.unpack_from("<i", buf, o)
+    o += 4
+    for _ in range(n_tok):
+        (ln,) = struct.unpack_from("<I", buf, o)
+        o += 4 + ln
+    out = {}
+    while o < len(buf):
+        nd, nl, tt = struct.unpack_from("<3i", buf, o)
+        o += 12
+        ne = struct.unpack_from(f"<{nd}i", buf, o)
+        o += 4 * nd
+        name = buf[o:o + nl].decode()
+        o += nl
+        nel = int(np.prod(ne))
+        nbytes = nel * 4 if tt == 0 else nel * 2 if tt == 1 else nel // 32 * BLOCK_BYTES[tt]
+        out[name] = (tt, ne, buf[o:o + nbytes])
+        o += nbytes
+    return out
+
+
+def quantize_rows(x: np.ndarray, qtype: str) -> bytes:
+    """ggml's quantize_row_*_reference over the rows of x (row length % 32 == 0), vectorised."""
+    b = x.astype(np.float32).reshape(-1, 32)
+    nb = b.shape[0]
+    if qtype in ("q5_0", "q4_0"):
+        nmax = 16 if qtype == "q5_0" else 8
+        am = np.abs(b).argmax(1)
+        mx = b[np.arange(nb), am]
+        d = mx / -nmax
+        idd = np.where(d != 0, 1.0 / np.where(d != 0, d, 1), 0).astype(np.float32)
+        q = np.minimum(2 * nmax - 1, (b * idd[:, None] + np.float32(nmax + 0.5)).astype(np.int8)).astype(np.int32)
+        dh = d.astype(np.float16).view(np.uint16)
+    elif qtype in ("q5_1", "q4_1"):
+        lo, hi = b.min(1), b.max(1)
+        d = (hi - lo) / (31 if qtype == "q5_1" else 15)
+        idd = np.where(d != 0, 1.0 / np.where(d != 0, d, 1), 0).astype(np.float32)
+        q = ((b - lo[:, None]) * idd[:, None] + np.float32(0.5)).astype(np.uint8).astype(np.int32)
+        q = np.minimum(q, 31 if qtype == "q5_1" else 15)
+        dh = d.astype(np.float16).view(np.uint16)
+        mh = lo.astype(np.float16).view(np.uint16)
+    else:  # q8_0
+        amax = np.abs(b).max(1)
+        d = amax / 127
+        idd = np.where(d != 0, 1.0 / np.where(d != 0, d, 1), 0).astype(np.float32)
+        q = np.round(b * idd[:, None]).astype(np.int8)
+        dh = d.astype(np.float16).view(np.uint16)
+        return b"".join(dh[i].tobytes() + q[i].tobytes() for i in range(nb))
+    qs = ((q[:, :16] & 0x0F) | ((q[:, 16:] & 0x0F) << 4)).astype(np.uint8)
+    out = []
+    if qtype in ("q5_0", "q5_1"):
+        hb = ((q >> 4) & 1).astype(np.uint64)
+        qh = (hb << np.arange(32, dtype=np.uint64)).sum(1).astype(np.uint32)
+    for i in range(nb):
+        rec = dh[i].tobytes()
+        if qtype in ("q5_1", "q4_1"):
+            rec += mh[i].tobytes()
+        if qtype in ("q5_0", "q5_1"):
+            rec += qh[i].tobytes()
+        out.append(rec + qs[i].tobytes())
+    return b"".join(out)
+
+
+def dequantize_rows(raw: bytes, qtype: str, n: int) -> np.ndarray:
+    """ggml's dequantize_row_* (f32 results: q*d (+ m), the product exact in f32)."""
+    bs = {"q4_0": 18, "q4_1": 20, "q5_0": 22, "q5_1": 24, "q8_0": 34}[qtype]
+    a = np.frombuffer(raw, np.uint8).reshape(-1, bs)
+    d = a[:, 0:2].copy().view(np.float16).astype(np.float32)[:, 0]
+    if qtype == "q8_0":
+        return (a[:, 2:].view(np.int8).astype(np.float32) * d[:, None]).reshape(-1)[:n]
+    off = 2
+    m = None
+    if qtype in ("q5_1", "q4_1"):
+        m = a[:, 2:4].copy().view(np.float16).astype(np.float32)[:, 0]
+        off = 4
+    qh = None
+    if qtype in ("q5_0", "q5_1"):
+        qh = a[:, off:off + 4].copy().view(np.uint32)[:, 0].astype(np.uint64)
+        off += 4
+    qs = a[:, off:off + 16].astype(np.int32)
+    q = np.concatenate([qs & 0x0F, qs >> 4], 1)
+    if qh is not None:
+        q = q | ((((qh[:, None] >> np.arange(32, dtype=np.uint64)) & 1).astype(np.int32)) << 4)
+    if m is None:
+        q = q - (16 if qtype == "q5_0" else 8)
+        y = q.astype(np.float32) * d[:, None]
+    else:
+        y = q.astype(np.float32) * d[:, None] + m[:, None]
+    return y.reshape(-1)[:n]
+
+
+def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, qtype: str | None = None) -> dict:
     """Write a seeded synthetic model. Returns the hparams dict. ftype 1 = f16 matrices, 0 = all f32.
-    shape may carry the "+conf" suffix (see CONF_SCALE)."""
+    shape may carry the "+conf" suffix (see CONF_SCALE) and a "+q5_0" / "+q5_1" / "+q8_0" / "+q4_0" /
+    "+q4_1" suffix: every 2-D tensor but QUANT_SKIP quantized as whisper.cpp's quantize tool does."""
+    for q in GGML_TYPES:
+        if shape.endswith("+" + q):
+            shape, qtype = shape[:-len(q) - 1], q
     conf = shape.endswith("+conf")
     n_vocab, n_mels, d, h, n_enc, n_dec = SHAPES[shape[:-5] if conf else shape]
     rng = np.random.default_rng(seed)
     hp = dict(n_vocab=n_vocab, n_audio_ctx=N_AUDIO_CTX, n_audio_state=d, n_audio_head=h,
               n_audio_layer=n_enc, n_text_ctx=N_TEXT_CTX, n_text_state=d, n_text_head=h,
-              n_text_layer=n_dec, n_mels=n_mels, ftype=ftype)
+              n_text_layer=n_dec, n_mels=n_mels,
+              ftype=ftype if qtype is None else GGML_FTYPES[qtype] + 1000 * GGML_QNT_VERSION)
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
         f.write(struct.pack("<I", GGML_MAGIC))
@@ -262,11 +380,16 @@ def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1) -
             if conf:
                 data = conf_adjust(name, data, n_vocab)
             use_f16 = (ftype == 1) and not is_f32
+            quant = qtype is not None and len(shp) == 2 and name not in QUANT_SKIP
             nb = name.encode()
-            f.write(struct.pack("<3i", len(shp), len(nb), 1 if use_f16 else 0))
+            ttype = GGML_TYPES[qtype] if quant else (1 if use_f16 else 0)
+            f.write(struct.pack("<3i", len(shp), len(nb), ttype))
             f.write(struct.pack(f"<{len(shp)}i", *reversed(shp)))
             f.write(nb)
-            f.write(data.astype("<f2" if use_f16 else "<f4").tobytes())
+            if quant:
+                f.write(quantize_rows(data, qtype))
+            else:
+                f.write(data.astype("<f2" if use_f16 else "<f4").tobytes())
     os.replace(tmp, path)
     return hp
 
@@ -305,7 +428,7 @@ def synthetic_pcm(k: int, seconds: float = 30.0, sr: int = 16000) -> np.ndarray:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
-    ap.add_argument("--shape", default="tiny", choices=sorted(SHAPES) + [k + "+conf" for k in sorted(SHAPES)])
+    ap.add_argument("--shape", default="tiny", help="a SHAPES key, optionally +conf and/or +q5_0 / +q5_1 / +q8_0 / +q4_0 / +q4_1")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--ftype", type=int, default=1)
     a = ap.parse_args()
