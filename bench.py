@@ -214,6 +214,67 @@ def plan(rank: int, world: int, args) -> None:
         print(json.dumps({"world": world, "max_elapsed": t, "shards": shards}), flush=True)
 
 
+def bench_frontend(wrs, ctx, buf, nb: int, n: int, reps: int = 5) -> dict:
+    """The reference's audio front-end (src-tauri/src/audio.rs) on this rank's chunks, device-resident:
+    find_silence_boundaries over the nb 16 kHz chunks (HBM-bound: 4 B per sample), and
+    resample_chunk of nb 30 s 48 kHz captures (f32 VALU-bound: 4 * fsi * fso FLOP per 171-sample
+    output block). Host wall clock around the synchronous C-ABI calls, best of `reps`."""
+    import numpy as np
+    L = wrs.lib()
+    dev = ctx.gpu_device
+    ptrs = (C.c_void_p * nb)(*[buf + i * n * 4 for i in range(nb)])
+    ns = (C.c_int * nb)(*([n] * nb))
+    cap = n // 16000 + 2
+    counts = np.zeros(nb, np.int32)
+    bnd = np.zeros((nb, cap), np.int32)
+    ip = C.POINTER(C.c_int)
+
+    def vad():
+        assert L.whisper_mi355x_find_silence_boundaries(dev, ptrs, ns, nb, 16000, True, counts.ctypes.data_as(ip),
+                                                        bnd.ctypes.data_as(ip), cap, None, None, 0) == 0
+    vad()
+    t_vad = min(_wall(vad) for _ in range(reps))
+    rate, n48 = 48000, 48000 * 30
+    n16 = L.whisper_mi355x_resample_len(n48, rate)
+    src = L.whisper_mi355x_dev_alloc(ctx.ptr, nb * n48 * 4)
+    dst = L.whisper_mi355x_dev_alloc(ctx.ptr, nb * n16 * 4)
+    assert src and dst
+    from make_model import synthetic_pcm
+    host = synthetic_pcm(0, seconds=30.0, sr=rate).astype(np.float32)
+    for i in range(nb):
+        L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(src + i * n48 * 4), host.ctypes.data, n48 * 4, 1)
+    iptr = (C.c_void_p * nb)(*[src + i * n48 * 4 for i in range(nb)])
+    optr = (C.c_void_p * nb)(*[dst + i * n16 * 4 for i in range(nb)])
+    nin = (C.c_int * nb)(*([n48] * nb))
+
+    def rs():
+        assert L.whisper_mi355x_resample_chunk(dev, iptr, nin, nb, rate, True, optr) == 0
+    rs()
+    t_rs = min(_wall(rs) for _ in range(reps))
+    L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(src))
+    L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(dst))
+    fsi, fso = C.c_int(), C.c_int()
+    L.whisper_mi355x_resample_operator(rate, C.byref(fsi), C.byref(fso), None, 0)
+    flops = nb * (-(-n16 // fso.value)) * 4.0 * fsi.value * fso.value
+    vad_bytes = nb * n * 4.0
+    return {
+        "clips": nb, "vad_boundaries_per_clip": float(counts.mean()),
+        "find_silence_boundaries": dict(ms=round(t_vad * 1e3, 3), audio_s_per_s=round(30.0 * nb / t_vad, 1),
+                                        gb_s=round(vad_bytes / t_vad / 1e9, 1),
+                                        hbm_frac=round(vad_bytes / t_vad / 1e9 / HBM_PEAK_GBS, 4)),
+        "resample_48k_to_16k": dict(ms=round(t_rs * 1e3, 3), audio_s_per_s=round(30.0 * nb / t_rs, 1),
+                                    tflop_s=round(flops / t_rs / 1e12, 2),
+                                    note="f32 VALU operator product (rubato FftFixedIn folded); wall clock "
+                                         "around the synchronous call incl. pointer-table uploads"),
+    }
+
+
+def _wall(fn) -> float:
+    t = time.perf_counter()
+    fn()
+    return time.perf_counter() - t
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +289,8 @@ def main():
     ap.add_argument("--variants", type=int, default=1,
                     help="also time the reference's prompted (default vocabulary) and auto-language workloads")
     ap.add_argument("--variant-steps", type=int, default=3)
+    ap.add_argument("--frontend", type=int, default=1,
+                    help="also time the GPU audio front-end (audio.rs VAD chunking + 48 kHz -> 16 kHz resampler)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this job's CPU share (OMP_NUM_THREADS)")
     ap.add_argument("--model-dir", default=os.environ.get("NW_MODEL_DIR", "/tmp/nw_models"))
@@ -360,6 +423,10 @@ def main():
                                  prompt_tokens=len(ctx.tokenize(wrs.DEFAULT_VOCABULARY)) if "vocabulary" in name else 0,
                                  phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
 
+    frontend = None
+    if args.frontend and rank == 0 and nb:
+        frontend = bench_frontend(wrs, ctx, buf, nb, n)
+
     if rank == 0:
         audio_s = 30.0 * global_batch * args.steps
         value = audio_s / elapsed
@@ -424,7 +491,7 @@ def main():
             "extra": {"rtf_inverse_per_gpu": round(value / world, 2), "decoded_tokens_per_step": decoded,
                       "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
                       "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),
-                      "weight_broadcast_s": round(bcast_s, 3)},
+                      "weight_broadcast_s": round(bcast_s, 3), "frontend": frontend},
         }
         print(json.dumps(line), flush=True)
     L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(buf))

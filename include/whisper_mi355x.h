@@ -127,6 +127,30 @@ WHISPER_API int whisper_mi355x_debug_xattn(struct whisper_context * ctx, const v
                                            int n, int n_ctx, int d, float scale, int splits, float rescale_thr,
                                            void * out, int reps, float * ms);
 
+/* Audio front-end on the GPU (src-tauri/src/audio.rs), for n_clips clips at
+ * once on HIP device `device`. pcm / audio / out point at host buffers, or (on_device = true) at
+ * buffers already in that device's HBM.
+ *
+ * whisper_mi355x_find_silence_boundaries replaces audio.rs:400-467 find_silence_boundaries(audio,
+ * sample_rate) (with estimate_noise_floor, audio.rs:373-397): counts[c] = number of split points of
+ * clip c (only the first `cap` are stored, boundaries[c * cap + i], sample indices); noise_floor[c]
+ * (optional) = the adaptive noise floor; rms_out (optional, [n_clips][rms_stride]) = the RMS of
+ * every 20 ms window, bit-identical to audio.rs:364-370 calculate_rms. Returns 0, or -1 on bad
+ * arguments. split_at_silences (audio.rs:469-507) is pure indexing and stays with the caller. */
+WHISPER_API int whisper_mi355x_find_silence_boundaries(int device, const float * const * pcm, const int * n_samples,
+                                                       int n_clips, int sample_rate, bool pcm_on_device, int * counts,
+                                                       int * boundaries, int cap, float * noise_floor, float * rms_out,
+                                                       int rms_stride);
+/* audio.rs:331-337 resample_chunk(audio, input_sample_rate) -> 16 kHz (audio.rs:509-563: rubato 0.15.0
+ * FftFixedIn, 1024-sample chunks, 2 sub-chunks, last chunk zero-padded, output truncated to
+ * len * 16000 / rate). out[c] must hold whisper_mi355x_resample_len(n_in[c], rate_in) floats. */
+WHISPER_API int whisper_mi355x_resample_len(int n_in, int rate_in);
+WHISPER_API int whisper_mi355x_resample_chunk(int device, const float * const * audio, const int * n_in, int n_clips,
+                                              int rate_in, bool on_device, float * const * out);
+/* The resampler's FFT pipeline as one linear map (tests): block sizes fsi / fso of rate_in, and
+ * W [2*fsi][fso] with output block m = sum_t x[(m-1)*fsi + t] W[t][:]. */
+WHISPER_API int whisper_mi355x_resample_operator(int rate_in, int * fsi, int * fso, float * W, long cap);
+
 /* ABI self-description, no device needed: sizeof(whisper_full_params), sizeof(whisper_context_params),
  * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /
  * new_segment_callback / vad_params). Lets a binding (bindgen, ctypes) be checked field-by-field. */

@@ -11,6 +11,15 @@ void launch_mel(const float* const* d_pcm, const int* d_n, const void* d_tab, co
 void launch_mel_window(DType dt, float* const* d_mel, const int* d_nlen, const int* d_n, const int* d_max,
                        const int* d_win_job, const int* d_win_seek, int n_win, int n_mel, void* out, hipStream_t st);
 void launch_mel_normalize(const float* d_mel, int nl, int n_samples, const int* d_max, int n_mel, float* out, hipStream_t st);
+// ---- audio front-end (kernels/audio.hip; audio.rs VAD chunking + resampler) ------------------------
+// rms[c][w] (row stride rms_stride >= max_n / (rate/50)) of every 20 ms window, then per clip the
+// noise floor (floor_out, optional) and the silence boundaries: counts[c], bounds[c][cap]
+void launch_silence_boundaries(const float* const* pcm, const int* n_samples, int n_clips, int max_n, int sample_rate,
+                               float* rms, int rms_stride, int* counts, int* bounds, int cap, float* floor_out,
+                               hipStream_t st);
+// out[c][m*fso + j] = sum_t in[c][(m-1)*fsi + t] * W[t][j] for m*fso + j < n_out[c]; W [2*fsi][ldw]
+void launch_resample(const float* const* in, const int* n_in, int n_clips, int max_out, const float* W, int ldw, int fsi,
+                     int fso, float* const* out, const int* n_out, hipStream_t st);
 
 // ---- layer norm / embedding (kernels/norm.hip) ------------------------------------------------
 // y[i] = LN(x[row(i)]) * w + b, x f32 [.][D] (row stride D), y T [M][D]; row(i) = rows ? rows[i] : i

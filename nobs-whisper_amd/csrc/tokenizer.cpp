@@ -3,6 +3,10 @@
 // whisper.cpp's own tokenizer [ext `tokenize`]: a GPT-2 style regex pre-split followed by greedy
 // longest-prefix matching against the model file's vocabulary (no BPE merges). Host-side: the
 // prompt is at most a few hundred bytes per call.
+//
+// Attribution: the pre-split regex and the longest-prefix loop follow whisper.cpp's `tokenize()`
+// (https://github.com/ggerganov/whisper.cpp, MIT License, Copyright (c) 2023-2024 The ggml
+// authors); bit-exact prompt token ids require the same std::regex semantics.
 #include <regex>
 
 #include "engine.h"

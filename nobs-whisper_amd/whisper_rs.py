@@ -166,6 +166,12 @@ def lib() -> C.CDLL:
         "whisper_mi355x_abi_layout": (C.c_int, [C.POINTER(C.c_size_t)]),
         "whisper_mi355x_kernel_timing": (C.c_int, [vp, C.c_int]),
         "whisper_mi355x_kernel_stats": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
+        "whisper_mi355x_find_silence_boundaries": (C.c_int, [C.c_int, C.POINTER(vp), ip, C.c_int, C.c_int, C.c_bool,
+                                                             ip, ip, C.c_int, fp, fp, C.c_int]),
+        "whisper_mi355x_resample_len": (C.c_int, [C.c_int, C.c_int]),
+        "whisper_mi355x_resample_chunk": (C.c_int, [C.c_int, C.POINTER(vp), ip, C.c_int, C.c_int, C.c_bool,
+                                                    C.POINTER(vp)]),
+        "whisper_mi355x_resample_operator": (C.c_int, [C.c_int, ip, ip, fp, C.c_long]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -211,6 +217,7 @@ class WhisperContext:
         cp.use_gpu = True
         cp.gpu_device = gpu_device
         self.L = L
+        self.gpu_device = gpu_device
         self.ptr = L.whisper_mi355x_init(path.encode(), cp, dtype, load_weights)
         if not self.ptr:
             raise RuntimeError(f"whisper_mi355x_init failed for {path}")
@@ -223,6 +230,7 @@ class WhisperContext:
         cp = L.whisper_context_default_params()
         cp.use_gpu = use_gpu
         self.L = L
+        self.gpu_device = cp.gpu_device
         self.ptr = L.whisper_init_from_file_with_params_no_state(path.encode(), cp)
         if not self.ptr:
             raise RuntimeError(f"failed to load {path}")
@@ -420,3 +428,90 @@ def filter_hallucinations(text: str) -> str:
     n = L.nobs_filter_hallucinations(text.encode(), buf, len(buf))
     assert n >= 0
     return buf.value.decode()
+
+
+# ---- audio.rs mirror (src-tauri/src/audio.rs) over the GPU front-end ---------------------------------
+WHISPER_SAMPLE_RATE = 16000   # audio.rs:7
+CHUNK_OVERLAP_MS = 200        # audio.rs:15
+MIN_CHUNK_DURATION_MS = 1000  # audio.rs:343
+
+
+def _ptr_table(arrays):
+    import numpy as np
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in arrays]
+    tab = (C.c_void_p * max(1, len(arrs)))(*[a.ctypes.data for a in arrs])
+    n = (C.c_int * max(1, len(arrs)))(*[len(a) for a in arrs])
+    return arrs, tab, n
+
+
+def find_silence_boundaries_batch(clips, sample_rate: int, device: int = 0, with_rms: bool = False):
+    """audio.rs:400-467 for every clip at once on the GPU: (boundaries per clip, noise floors, and
+    with_rms the 20 ms window RMS rows)."""
+    import numpy as np
+    arrs, tab, n = _ptr_table(clips)
+    nc = len(arrs)
+    if nc == 0:
+        return ([], [], []) if with_rms else ([], [])
+    min_chunk = sample_rate * MIN_CHUNK_DURATION_MS // 1000
+    cap = max(len(a) for a in arrs) // max(1, min_chunk) + 2
+    counts = np.zeros(nc, np.int32)
+    b = np.zeros((nc, cap), np.int32)
+    nf = np.zeros(nc, np.float32)
+    ws = sample_rate // 50
+    stride = max(1, max(len(a) for a in arrs) // ws)
+    rms = np.zeros((nc, stride), np.float32) if with_rms else None
+    ip, fp = C.POINTER(C.c_int), C.POINTER(C.c_float)
+    rc = lib().whisper_mi355x_find_silence_boundaries(
+        device, tab, n, nc, sample_rate, False, counts.ctypes.data_as(ip), b.ctypes.data_as(ip), cap,
+        nf.ctypes.data_as(fp), rms.ctypes.data_as(fp) if with_rms else None, stride)
+    if rc != 0:
+        raise RuntimeError(f"whisper_mi355x_find_silence_boundaries: {rc}")
+    bounds = [b[c, :counts[c]].tolist() for c in range(nc)]
+    if with_rms:
+        return bounds, nf.tolist(), [rms[c, :len(arrs[c]) // ws].copy() for c in range(nc)]
+    return bounds, nf.tolist()
+
+
+def find_silence_boundaries(audio, sample_rate: int, device: int = 0) -> list:
+    """audio.rs:400 find_silence_boundaries(audio, sample_rate) -> Vec<usize>."""
+    return find_silence_boundaries_batch([audio], sample_rate, device)[0][0]
+
+
+def split_at_silences_with_overlap(audio, boundaries, sample_rate: int) -> list:
+    """audio.rs:474-507: chunks audio[max(start - overlap, 0) : boundary], overlap 200 ms."""
+    if not boundaries:
+        return [audio[:]]
+    overlap = sample_rate * CHUNK_OVERLAP_MS // 1000
+    chunks, start = [], 0
+    for b in boundaries:
+        if start < b < len(audio):
+            chunks.append(audio[max(start - overlap, 0):b])
+            start = b
+    if start < len(audio):
+        chunks.append(audio[max(start - overlap, 0):])
+    return chunks
+
+
+def split_at_silences(audio, boundaries) -> list:
+    """audio.rs:469-471."""
+    return split_at_silences_with_overlap(audio, boundaries, WHISPER_SAMPLE_RATE)
+
+
+def resample_batch(clips, input_sample_rate: int, device: int = 0) -> list:
+    """audio.rs:331-337 resample_chunk for every clip at once on the GPU."""
+    import numpy as np
+    arrs, tab, n = _ptr_table(clips)
+    if not arrs:
+        return []
+    L = lib()
+    outs = [np.zeros(max(1, L.whisper_mi355x_resample_len(len(a), input_sample_rate)), np.float32) for a in arrs]
+    otab = (C.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+    rc = L.whisper_mi355x_resample_chunk(device, tab, n, len(arrs), input_sample_rate, False, otab)
+    if rc != 0:
+        raise RuntimeError(f"whisper_mi355x_resample_chunk: {rc}")
+    return [o[:L.whisper_mi355x_resample_len(len(a), input_sample_rate)] for o, a in zip(outs, arrs)]
+
+
+def resample_chunk(audio, input_sample_rate: int, device: int = 0):
+    """audio.rs:331 resample_chunk(audio, input_sample_rate) -> Vec<f32> at 16 kHz."""
+    return resample_batch([audio], input_sample_rate, device)[0]

@@ -102,6 +102,11 @@ def lib():
             "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
             "oracle_mel_tables": (None, [fp, fp, fp]),
             "oracle_tensor": (C.c_long, [vp, C.c_char_p, C.c_int, fp, C.c_long]),
+            "oracle_calculate_rms": (C.c_float, [fp, C.c_int]),
+            "oracle_estimate_noise_floor": (C.c_float, [fp, C.c_int, C.c_int]),
+            "oracle_find_silence_boundaries": (C.c_int, [fp, C.c_int, C.c_int, ip, C.c_int]),
+            "oracle_split_at_silences": (C.c_int, [C.c_int, ip, C.c_int, C.c_int, ip, ip, C.c_int]),
+            "oracle_resample": (C.c_int, [fp, C.c_int, C.c_int, fp, C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -225,3 +230,38 @@ class Oracle:
         return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
                     no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins, seq=list(seq[:n_seq]),
                     decisions=decisions_to_dicts(dec[:nd]))
+
+
+# ---- audio.rs restatement (oracle/oracle_audio.cpp) -------------------------------------------------
+def calculate_rms(x) -> float:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    return float(lib().oracle_calculate_rms(_fp(x), len(x)))
+
+
+def estimate_noise_floor(x, sr: int) -> float:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    return float(lib().oracle_estimate_noise_floor(_fp(x), len(x), sr))
+
+
+def find_silence_boundaries(x, sr: int) -> list:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    cap = len(x) // max(1, sr) + 2
+    out = np.zeros(cap, np.int32)
+    n = lib().oracle_find_silence_boundaries(_fp(x), len(x), sr, _ip(out), cap)
+    return out[:n].tolist()
+
+
+def split_at_silences(n: int, bounds, sr: int) -> list:
+    b = np.ascontiguousarray(bounds, dtype=np.int32)
+    cap = len(b) + 2
+    s, e = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    k = lib().oracle_split_at_silences(n, _ip(b), len(b), sr, _ip(s), _ip(e), cap)
+    return list(zip(s[:k].tolist(), e[:k].tolist()))
+
+
+def resample(x, rate_in: int) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    cap = int(len(x) * 16000 / rate_in) + 2048
+    out = np.zeros(max(cap, 1), np.float32)
+    n = lib().oracle_resample(_fp(x), len(x), rate_in, _fp(out), cap)
+    return out[:n].copy()
