@@ -709,15 +709,38 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     const lds_u16_t ltab = (lds_u16_t)(const void*)ltab_g;
+    const int row = lane >> 2, c0 = (lane & 3) * 16;
+    // EPI_RESID: the residual row segment of sub-tile i + 1 is loaded while sub-tile i is staged and
+    // stored (a load -> add -> store chain per sub-tile left eight memory latencies in a row)
+    auto resid_ptr = [&](int i) -> float* {
+        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        float* p = (float*)g.out + (long)m * g.ldo + n;
+        return (m < g.M && n + 16 <= g.N && (((uintptr_t)p) & 15) == 0) ? p : nullptr;
+    };
+    float4 rx[4];
+    if constexpr (EPI == EPI_RESID) {
+        const float* p = resid_ptr(0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) rx[k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
+        float4 cur[4];
+        if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) cur[k] = rx[k];
+            if (i + 1 < 8) {
+                const float* p = resid_ptr(i + 1);
+#pragma unroll
+                for (int k = 0; k < 4; k++) rx[k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++) stg[((lane >> 4) * 4 + r) * LDW + j * 16 + (lane & 15)] = acc[i][j][r];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        const int row = lane >> 2, c0 = (lane & 3) * 16;
         float v[16];
 #pragma unroll
         for (int k = 0; k < 16; k += 4) {
@@ -727,6 +750,22 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if constexpr (EPI == EPI_RESID) {
+            float* p = resid_ptr(i);
+            if (p) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int c = 4 * k;
+                    if (g.bias) {
+                        const float4 b = *(const float4*)(g.bias + n + c);
+                        v[c] = v[c] + b.x; v[c + 1] = v[c + 1] + b.y; v[c + 2] = v[c + 2] + b.z; v[c + 3] = v[c + 3] + b.w;
+                    }
+                    ((float4*)p)[k] = make_float4(v[c] + cur[k].x, v[c + 1] + cur[k].y, v[c + 2] + cur[k].z,
+                                                  v[c + 3] + cur[k].w);
+                }
+                continue;
+            }
+        }
         if (m < g.M && n < g.N) epilogue16<EPI, T, LT>(g, m, n, v, ltab);
     }
 }

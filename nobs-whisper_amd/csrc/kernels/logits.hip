@@ -1,6 +1,6 @@
 // Device-side whisper_process_logits + whisper_sample_token(best=true).
 //
-// One 1024-thread workgroup per sequence reads its logits row (V = 51864..51866 f32) four times
+// One 1024-thread workgroup per sequence reads its logits row (V = 51864..51866 f32) once, into
 // from L2 and returns only a TokOut record (token id, p, plog, tid, pt, ptsum, no-speech prob),
 // so the host never copies a [B, V] logits block per step. Rules, in whisper.cpp's order [ext]:
 // temperature divide; suppress_blank (initial step: EOT and " "); <|notimestamps|>; optional
@@ -17,8 +17,7 @@ namespace wm {
 
 static constexpr int LT = 1024;
 
-__device__ __forceinline__ float masked_logit(const float* L, int i, const SeqCtl& c, const VocabIds& v) {
-    float x = L[i];
+__device__ __forceinline__ float masked_logit(float x, int i, const SeqCtl& c, const VocabIds& v) {
     if (c.temperature > 0.0f) x = x / c.temperature;
     if (c.suppress_blank && c.is_initial && (i == v.eot || i == v.space)) return -INFINITY;
     if (i == v.not_) return -INFINITY;
@@ -81,6 +80,24 @@ __device__ void block_argmax(float& v, int& idx, float* shv, int* shi) {
         if (shv[i] > v || (shv[i] == v && shi[i] < idx)) { v = shv[i]; idx = shi[i]; }
 }
 
+// The row is loaded once into registers (NPT values per thread, all loads issued back to back) and
+// every pass works on registers: a row re-read per pass from L2 with one load in flight per wave
+// made the kernel latency-bound (128 us per step at 128 rows). Per-thread accumulation runs over
+// i = tid, tid + LT, ... in ascending order, as before (same bits).
+static constexpr int NPT = 51;  // 51 * 1024 >= 51866 (largest Whisper vocabulary)
+static constexpr int NPT_LDS = 36;  // values k < NPT_LDS of each thread live in LDS (144 KiB), the rest in VGPRs
+
+// element k of this thread's row slice (compile-time k after unrolling: LDS or a register)
+struct RowSlice {
+    float* lds;
+    float reg[NPT - NPT_LDS];
+    __device__ __forceinline__ float get(int k) const { return k < NPT_LDS ? lds[k * LT + threadIdx.x] : reg[k - NPT_LDS]; }
+    __device__ __forceinline__ void set(int k, float v) {
+        if (k < NPT_LDS) lds[k * LT + threadIdx.x] = v;
+        else reg[k - NPT_LDS] = v;
+    }
+};
+
 __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ logits, long ld, const SeqCtl* __restrict__ ctl,
                                                     VocabIds v, TokOut* __restrict__ out, float* __restrict__ probs) {
     const int s = blockIdx.x;
@@ -91,41 +108,61 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
     __shared__ int shi[LT / 64];
     __shared__ double shd[LT / 64];
 
+    extern __shared__ float s_row[];  // [NPT_LDS][LT]
+    RowSlice x{s_row};
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = tid + k * LT;
+        x.set(k, i < n ? L[i] : -INFINITY);
+    }
     float nosp_prob = 0.0f;
     if (c.want_nosp) {  // no-speech probability from the raw (unfiltered) logits
         float mx = -INFINITY;
-        for (int i = tid; i < n; i += LT) mx = fmaxf(mx, L[i]);
+#pragma unroll
+        for (int k = 0; k < NPT; k++)
+            if (tid + k * LT < n) mx = fmaxf(mx, x.get(k));
         mx = block_max(mx, shf);
         float sm = 0.0f;
-        for (int i = tid; i < n; i += LT) sm += expf(L[i] - mx);
+#pragma unroll
+        for (int k = 0; k < NPT; k++)
+            if (tid + k * LT < n) sm += expf(x.get(k) - mx);
         sm = block_sum(sm, shf);
         const float lse = logf(sm) + mx;
         nosp_prob = expf(L[v.nosp] - lse);
     }
+    // filtered logits, in place
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = tid + k * LT;
+        if (i < n) x.set(k, masked_logit(x.get(k), i, c, v));
+    }
     // log-softmax of the filtered logits
     float mx = -INFINITY;
-    for (int i = tid; i < n; i += LT) mx = fmaxf(mx, masked_logit(L, i, c, v));
+#pragma unroll
+    for (int k = 0; k < NPT; k++) mx = fmaxf(mx, x.get(k));
     mx = block_max(mx, shf);
     float sm = 0.0f;
-    for (int i = tid; i < n; i += LT) {
-        const float x = masked_logit(L, i, c, v);
-        if (x > -INFINITY) sm += expf(x - mx);
-    }
+#pragma unroll
+    for (int k = 0; k < NPT; k++)
+        if (x.get(k) > -INFINITY) sm += expf(x.get(k) - mx);
     sm = block_sum(sm, shf);
     const float lse = logf(sm) + mx;
     // timestamp rule
     float mts = -INFINITY, mtext = -INFINITY;
-    for (int i = tid; i < n; i += LT) {
-        const float x = masked_logit(L, i, c, v);
-        const float lp = x > -INFINITY ? x - lse : -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = tid + k * LT;
+        const float lp = x.get(k) > -INFINITY ? x.get(k) - lse : -INFINITY;
         if (i >= v.beg) mts = fmaxf(mts, lp); else mtext = fmaxf(mtext, lp);
     }
     mts = block_max(mts, shf);
     mtext = block_max(mtext, shf);
     float sts = 0.0f;
-    for (int i = v.beg + tid; i < n; i += LT) {
-        const float x = masked_logit(L, i, c, v);
-        const float lp = x > -INFINITY ? x - lse : -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = tid + k * LT;
+        if (i < v.beg) continue;
+        const float lp = x.get(k) > -INFINITY ? x.get(k) - lse : -INFINITY;
         if (lp > -INFINITY) sts += expf(lp - mts);
     }
     sts = block_sum(sts, shf);
@@ -135,13 +172,16 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
     float best = 0.0f, best_ts = 0.0f;
     int ibest = 0x7fffffff, its = 0x7fffffff;
     double sum_ts = 0.0;
-    for (int i = tid; i < n; i += LT) {
-        float x = masked_logit(L, i, c, v);
-        if (mask_text && i < v.beg) x = -INFINITY;
-        const float p = x == -INFINITY ? 0.0f : expf(x - lse);
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = tid + k * LT;
+        if (i >= n) continue;
+        float xv = x.get(k);
+        if (mask_text && i < v.beg) xv = -INFINITY;
+        const float p = xv == -INFINITY ? 0.0f : expf(xv - lse);
         if (c.want_probs) {  // [seq][2][V]: probs, logprobs (host sampling at t > 0)
             probs[(long)s * 2 * n + i] = p;
-            probs[(long)s * 2 * n + n + i] = x == -INFINITY ? -INFINITY : x - lse;
+            probs[(long)s * 2 * n + n + i] = xv == -INFINITY ? -INFINITY : xv - lse;
         }
         if (p > best) { best = p; ibest = i; }
         if (i >= v.beg) {
@@ -157,9 +197,9 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
         r.id = best > 0.0f ? ibest : 0;
         r.p = best;
         {
-            float x = masked_logit(L, r.id, c, v);
-            if (mask_text && r.id < v.beg) x = -INFINITY;
-            r.plog = x > -INFINITY ? x - lse : -INFINITY;
+            float xv = masked_logit(L[r.id], r.id, c, v);
+            if (mask_text && r.id < v.beg) xv = -INFINITY;
+            r.plog = xv > -INFINITY ? xv - lse : -INFINITY;
         }
         r.tid = best_ts > 0.0f ? its : 0;
         r.pt = (float)((double)best_ts / (sum_ts + 1e-10));
@@ -174,7 +214,8 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v, TokOut* out, float* probs,
                    hipStream_t st) {
     if (n_seq <= 0) return;
-    logits_kernel<<<n_seq, LT, 0, st>>>(logits, ld, ctl, v, out, probs);
+    if (v.n_vocab > NPT * LT) { fprintf(stderr, "whisper_mi355x: vocabulary %d > %d\n", v.n_vocab, NPT * LT); abort(); }
+    logits_kernel<<<n_seq, LT, (size_t)NPT_LDS * LT * sizeof(float), st>>>(logits, ld, ctl, v, out, probs);
 }
 
 }  // namespace wm

@@ -63,6 +63,32 @@ def test_gemm_matches_numpy(wrs, ctx, M, N, K, variant):
     assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
 
 
+@pytest.mark.parametrize("M,N,K", [(3005, 1280, 1280), (4096, 1280, 5120), (2053, 1088, 1280), (1500, 512, 2048),
+                                   (128, 1280, 5120), (37, 384, 1536)])
+def test_gemm_resid_epilogue(wrs, ctx, M, N, K):
+    """EPI_RESID (x += A.B^T + bias, f32 residual in place) on the big-tile path (prefetched residual
+    loads) and the decode path, with a random initial residual and ragged M / N edges."""
+    L = wrs.lib()
+    rng = np.random.default_rng(M + 3 * N + K)
+    A = rng.standard_normal((M, K)).astype(np.float16)
+    B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    x0 = rng.standard_normal((M, N)).astype(np.float32)
+    pa, pb, pbias, px = _dev(wrs, ctx, A), _dev(wrs, ctx, B), _dev(wrs, ctx, bias), _dev(wrs, ctx, x0)
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_gemm(ctx.ptr, 2, C.c_void_p(pa), M, K, C.c_void_p(pb), N, C.c_void_p(pbias),
+                                       C.c_void_p(px), 1, C.byref(ms)) == 0
+    out = np.empty_like(x0)
+    L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(px), out.nbytes, 2)
+    for p in (pa, pb, pbias, px):
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    A64, B64 = A.astype(np.float64), B.astype(np.float64)
+    ref = x0 + A64 @ B64.T + bias
+    bound = 1e-4 * (np.abs(A64) @ np.abs(B64).T) + 1e-5 + 1e-6 * np.abs(x0)
+    err = np.abs(out - ref)
+    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (37, 384, 1536), (128, 1280, 5120), (128, 1280, 1280), (64, 1024, 4096)])
 def test_gemm_resid_ln_matches_numpy(wrs, ctx, M, N, K):
     """Decode-step residual GEMM + fused LayerNorm (split-K slabs -> reduce + residual + LN)."""
