@@ -546,6 +546,21 @@ int whisper_mi355x_debug_gemm_fp8(struct whisper_context* ctx, int epi, const vo
     hipStreamDestroy(st);
     return 0;
 }
+int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale,
+                                     void* mx_scale, int M, int K, const void* B8, const float* b_scale, int N,
+                                     const float* bias, void* out) {
+    if (!ctx || !mx_scale) return -1;
+    hipSetDevice(ctx->c.device);
+    GemmArgs g{};
+    g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+    g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    g.mx_scale = (uint8_t*)mx_scale;
+    launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, nullptr);
+    WM_CHECK(hipDeviceSynchronize());
+    return 0;
+}
 int whisper_mi355x_debug_quant_fp8(struct whisper_context* ctx, const void* x, long rows, int K, void* q, float* s) {
     if (!ctx) return -1;
     hipSetDevice(ctx->c.device);

@@ -131,7 +131,7 @@ static void free_ws(Workspace& w) {
     // are freed with their parent
     void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
                   w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk,
-                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs, w.qtiles};
+                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs, w.mxs, w.qtiles};
     for (void* p : ps) dfree(p);
     if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
     if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
@@ -196,8 +196,10 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
     size_t unused = 0;
     if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
-        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job, (void*)w.hs}) dfree(p);
+        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job, (void*)w.hs, (void*)w.mxs})
+            dfree(p);
         w.hs = nullptr;
+        w.mxs = nullptr;
         WM_CHECK(hipMalloc(&w.mel_img, (size_t)n_enc * 3002 * nm * E));
         WM_CHECK(hipMalloc(&w.h1, (size_t)n_enc * 3002 * d * E));
         WM_CHECK(hipMemset(w.h1, 0, (size_t)n_enc * 3002 * d * E));  // conv padding rows stay zero
@@ -206,7 +208,10 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
         WM_CHECK(hipMalloc(&w.att, (size_t)n_enc * T * d * E));
         WM_CHECK(hipMalloc(&w.ff, (size_t)n_enc * T * 4 * d * E));
         WM_CHECK(hipMalloc((void**)&w.x, (size_t)n_enc * T * d * 4));
-        if (c->fp8_enc) WM_CHECK(hipMalloc((void**)&w.hs, (size_t)n_enc * T * sizeof(float)));
+        if (c->fp8_enc) {
+            WM_CHECK(hipMalloc((void**)&w.hs, (size_t)n_enc * T * sizeof(float)));
+            WM_CHECK(hipMalloc((void**)&w.mxs, (size_t)n_enc * T * (4 * d / 32)));
+        }
         WM_CHECK(hipMalloc((void**)&w.win_job, (size_t)n_enc * 3 * sizeof(int)));
         w.win_seek = w.win_job + n_enc;
         w.win_slot = w.win_job + 2 * n_enc;
@@ -383,6 +388,16 @@ static void ensure_fp8(Context* c) {
     c->fp8_ready = true;
 }
 
+// fp8 mode, FC1 -> FC2: MX hand-off (FC1's epilogue quantizes per 32-column block, no separate
+// quantizer pass over the GELU output). WHISPER_MI355X_FP8_MX=0 restores the per-row requantization.
+static bool fp8_mx() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_FP8_MX");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float* sa, const float* sb, hipStream_t st) {
     KT kt(s, K_GEMM_ENC, 2.0 * g.M * g.N * g.K, st);
     launch_gemm_fp8(s->ctx->dt, epi, g, sa, sb, st);
@@ -437,9 +452,20 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
                 }
                 tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
                 launch_layernorm_fp8(w.x, M, d, L.ln2_w, L.ln2_b, w.hn, w.hs, st);
-                tgemm_fp8(s, EPI_GELU_F, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
-                launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
-                tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
+                if (fp8_mx()) {
+                    // FC1 writes its GELU output as MX e4m3 (one E8M0 scale per row and 32-column
+                    // block) straight into the qkv buffer; FC2's block-scaled MFMA consumes the scales
+                    GemmArgs g1 = gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.qkv, 4 * d);
+                    g1.mx_scale = w.mxs;
+                    tgemm_fp8(s, EPI_GELU_MX, g1, w.hs, F.s1, st);
+                    GemmArgs g2 = gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d);
+                    g2.mx_scale = w.mxs;
+                    tgemm_fp8(s, EPI_RESID, g2, nullptr, F.s2, st);
+                } else {
+                    tgemm_fp8(s, EPI_GELU_F, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
+                    launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
+                    tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
+                }
                 continue;
             }
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln1_w, L.ln1_b, w.hn, st);

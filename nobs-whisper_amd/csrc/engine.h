@@ -114,6 +114,7 @@ struct Workspace {
     void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
     float* x = nullptr;
     float* hs = nullptr;  // fp8 encoder: per-row scales of the quantized GEMM inputs
+    uint8_t* mxs = nullptr;  // fp8 encoder: E8M0 block scales of the FC1 output [rows][4d/32]
     // caches (cap_jobs slots). In direct mode `cross` is allocated on first use (prompts too long
     // for the direct prefill) and cross_fresh[slot] says whether a slot's cross K/V match enc.
     void *cross = nullptr, *self = nullptr;

@@ -43,6 +43,8 @@ enum Epi : int {
     EPI_CROSSKV = 5,   // T scatter into cross cache [slot][L][2][H][ctx][64]; K columns scaled
     EPI_QKV_DEC = 6,   // n<d: T q[m][n]*scale ; d<=n<2d: K cache (scaled) ; 2d<=n<3d: V cache
     EPI_GELU_F = 7,    // T out = tanh-GELU by formula in f32 (fp8 mode only: not ggml's f16 table)
+    EPI_GELU_MX = 8,   // fp8 mode: GELU by formula, then MX e4m3: out bytes [M][N] = e4m3(v / 2^e) with one
+                       // power-of-two scale per row and 32-column block, mx_scale[m][n/32] = e + 127 (E8M0)
 };
 
 struct GemmArgs {
@@ -60,11 +62,16 @@ struct GemmArgs {
     // EPI_RESID on the split-K path only: fused LayerNorm of the updated residual rows,
     // ln_out[m][:] = LN(out[m][:]) * ln_w + ln_b (the next GEMM's input; null = no LN)
     const float* ln_w; const float* ln_b; void* ln_out;
+    // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
+    // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
+    uint8_t* mx_scale;
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
 // fp8 (OCP e4m3) operands with per-row f32 scales: C = (A8 . B8^T) * a_scale[m] * b_scale[n], then
-// the epilogue (EPI_STORE / EPI_GELU / EPI_RESID); K % 128 == 0, N % 16 == 0. A/B strides in bytes.
+// the epilogue (EPI_STORE / EPI_GELU / EPI_GELU_F / EPI_GELU_MX / EPI_RESID); K % 128 == 0,
+// N % 16 == 0 (% 32 for EPI_GELU_MX). A/B strides in bytes. a_scale == null: A is MX-scaled, its
+// E8M0 block scales in a.mx_scale [M][K/32] (the output of an EPI_GELU_MX launch).
 void launch_gemm_fp8(DType dt, int epi, const GemmArgs& a, const float* a_scale, const float* b_scale, hipStream_t st);
 // q[r][:] = e4m3(x[r][:] / s[r]), s[r] = max|x[r][:]| / 448 (x in the MFMA type, K % 8 == 0)
 void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, float* s, hipStream_t st);

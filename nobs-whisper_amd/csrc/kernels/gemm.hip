@@ -778,20 +778,25 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
 // rate). A K-tile is 128 elements = the same 128 bytes per row as the bf16 kernel's 64, so the
 // LDS image, swizzle, DMA schedule, barriers and counted waits are unchanged; one MFMA per
 // (fragment, K-tile) instead of two, i.e. half the K-tiles for the same MFMA cycles per tile.
-// A lane's 32 operand bytes are the two adjacent 16-byte chunks 2(l>>4), 2(l>>4)+1 of its row,
-// read identically for A and B: whatever k order the instruction assigns inside a lane, both
-// operands use the same one, so the dot product is over all 128 k of the tile.
+// A lane's 32 operand bytes are the 16-byte chunks (l>>4) and (l>>4)+4 of its row, read identically
+// for A and B, which is the instruction's own k order (see frag below).
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ f32x4 mfma_mx8(i32x8 a, i32x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 
-template <typename T, int EPI>
+// MXA: A carries MX block scales (E8M0 per row and 32-k block, g.mx_scale [M][K/32], the output of an
+// EPI_GELU_MX launch) instead of a per-row f32 scale: each K-tile's 4 scale bytes per row are staged
+// next to the A tile (one 4-byte LDS-DMA per lane of the first half-wave of every wave, issued with
+// the A stage so the counted waits still cover it) and handed to the block-scaled MFMA per lane (a
+// lane's 32 k values are one block).
+template <typename T, int EPI, bool MXA = false>
 __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const int tiles_n, const float* __restrict__ sa,
                                                         const float* __restrict__ sb) {
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int BM = 256, BK = 128;  // BK in fp8 elements = bytes
     __shared__ u32x4 lds[2][(BM + 256) * 8];
+    __shared__ uint32_t lsc[2][MXA ? BM : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
@@ -812,6 +817,9 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
             const int n = min(n0 + r, g.N - 1);
             b_src[h][i] = B + (long)n * g.K + c * 16;
         }
+    // MX scales of rows m0 + wave*32 + (lane & 31): one u32 (4 blocks = one K-tile) per row
+    const uint8_t* sc_src = nullptr;
+    if constexpr (MXA) sc_src = g.mx_scale + (long)min(m0 + wave * 32 + (lane & 31), g.M - 1) * (g.K / 32);
     auto stage_a = [&](int kt) {
         u32x4* st = &lds[kt & 1][0];
 #pragma unroll
@@ -820,6 +828,10 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
             for (int i = 0; i < 2; i++)
                 __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
+        if constexpr (MXA) {
+            if (lane < 32)
+                __builtin_amdgcn_global_load_lds((const void*)(sc_src + kt * 4), (lds_ptr_t)&lsc[kt & 1][wave * 32], 4, 0, 0);
+        }
     };
     auto stage_b = [&](int kt) {
         u32x4* st = &lds[kt & 1][BM * 8];
@@ -836,26 +848,40 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     i32x8 a0[4], a1[4], b0[2], b1[2];
+    int s0[4] = {127, 127, 127, 127}, s1[4] = {127, 127, 127, 127};  // MXA: E8M0 per A fragment (row, 32-k block)
+    // lane l's operand registers 0-3 / 4-7 hold k = 16(l>>4) + [0, 16) / 64 + 16(l>>4) + [0, 16) of the
+    // K-tile (probed on gfx950: tools/probe/mx_layout.hip), so the 16-byte chunks (l>>4) and
+    // (l>>4) + 4 of the row are loaded: instruction k == memory k, and a 32-k MX block (scale lane
+    // row + 16 * block) is 32 consecutive bytes of the row
     auto frag = [&](const u32x4* img, int row) -> i32x8 {
-        const int c0 = 2 * (lane >> 4), sw = (row >> 1) & 7;
-        const u32x4 x = img[row * 8 + (c0 ^ sw)], y = img[row * 8 + ((c0 + 1) ^ sw)];
+        const int c0 = lane >> 4, sw = (row >> 1) & 7;
+        const u32x4 x = img[row * 8 + (c0 ^ sw)], y = img[row * 8 + ((c0 + 4) ^ sw)];
         return (i32x8){(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
     };
-    auto read_a = [&](int buf, int mq, i32x8 (&af)[4]) {
+    auto read_a = [&](int buf, int mq, i32x8 (&af)[4], int (&sf)[4]) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) af[i] = frag(&lds[buf][0], wm * 128 + (mq * 4 + i) * 16 + (lane & 15));
+        for (int i = 0; i < 4; i++) {
+            const int r = wm * 128 + (mq * 4 + i) * 16 + (lane & 15);
+            af[i] = frag(&lds[buf][0], r);
+            if constexpr (MXA) sf[i] = (int)((lsc[buf][r] >> (8 * (lane >> 4))) & 0xFF);
+        }
     };
     auto read_b = [&](int buf, int nq, i32x8 (&bf)[2]) {
 #pragma unroll
         for (int j = 0; j < 2; j++) bf[j] = frag(&lds[buf][BM * 8], wn * 64 + (nq * 2 + j) * 16 + (lane & 15));
     };
-    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2]) {
+    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2], const int (&sf)[4]) {
         asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int j = 0; j < 2; j++) acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
+            for (int j = 0; j < 2; j++) {
+                if constexpr (MXA)
+                    acc[mq * 4 + i][nq * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                        af[i], bf[j], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0, sf[i], 0, 127);
+                else acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
+            }
         __builtin_amdgcn_s_setprio(0);
         asm volatile("s_barrier" ::: "memory");
     };
@@ -869,20 +895,20 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
         read_b(buf, 0, b0);
-        read_a(buf, 0, a0);
+        read_a(buf, 0, a0, s0);
         if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
-        mfma_q(0, 0, a0, b0);
+        mfma_q(0, 0, a0, b0, s0);
         read_b(buf, 1, b1);
-        mfma_q(0, 1, a0, b1);
-        read_a(buf, 1, a1);
-        mfma_q(1, 1, a1, b1);
+        mfma_q(0, 1, a0, b1, s0);
+        read_a(buf, 1, a1, s1);
+        mfma_q(1, 1, a1, b1, s1);
         if (kt + 2 < nk) {
             stage_b(kt + 2);
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        mfma_q(1, 0, a1, b0);
+        mfma_q(1, 0, a1, b0, s1);
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -920,8 +946,46 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if constexpr (EPI == EPI_GELU_MX) {
+            // lanes l, l^1 hold the two 16-column halves of one 32-column block of row m: every lane
+            // takes part in the DPP exchange (rows past M compute on clamped data, store nothing)
+            const float am = m < g.M ? (MXA ? 1.0f : sa[m]) : 0.0f;
+            float amax = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                float x = (v[k] * am) * bs[k];
+                if (g.bias) x = x + g.bias[min(n + k, g.N - 1)];
+                v[k] = gelu_formula(x);
+                amax = fmaxf(amax, fabsf(v[k]));
+            }
+            amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, amax), 0xB1, 0xF, 0xF, false)));
+            // power-of-two scale 2^e with amax / 2^e <= 448 (e = ceil(log2(amax / 448)))
+            int e = 0;
+            if (amax > 0.0f) {
+                int ex;
+                const float fr = frexpf(amax / 448.0f, &ex);
+                e = fr == 0.5f ? ex - 1 : ex;
+                e = max(-127, min(127, e));
+            }
+            const float inv = ldexpf(1.0f, -e);
+            if (m < g.M && n + 16 <= g.N) {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    int p = 0;
+                    p = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * q] * inv, -448.f), 448.f),
+                                                        fminf(fmaxf(v[4 * q + 1] * inv, -448.f), 448.f), p, false);
+                    p = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * q + 2] * inv, -448.f), 448.f),
+                                                        fminf(fmaxf(v[4 * q + 3] * inv, -448.f), 448.f), p, true);
+                    w[q] = (uint32_t)p;
+                }
+                *(u32x4*)((uint8_t*)g.out + (long)m * g.ldo + n) = (u32x4){w[0], w[1], w[2], w[3]};
+                if ((lane & 1) == 0) g.mx_scale[(long)m * (g.N / 32) + n / 32] = (uint8_t)(e + 127);
+            }
+            continue;
+        }
         if (m < g.M && n < g.N) {
-            const float am = sa[m];
+            const float am = MXA ? 1.0f : sa[m];
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = (v[k] * am) * bs[k];
             epilogue16<EPI, T, LT>(g, m, n, v, ltab);
@@ -1358,14 +1422,21 @@ static void launch_mx_t(int epi, const GemmArgs& g, const float* sa, const float
         case EPI_STORE: gemm8p_mx_kernel<T, EPI_STORE><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_GELU: gemm8p_mx_kernel<T, EPI_GELU><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_GELU_F: gemm8p_mx_kernel<T, EPI_GELU_F><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
-        case EPI_RESID: gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        case EPI_GELU_MX: gemm8p_mx_kernel<T, EPI_GELU_MX><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
+        case EPI_RESID:
+            if (sa) gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb);
+            else gemm8p_mx_kernel<T, EPI_RESID, true><<<grid, 512, 0, st>>>(g, tn, sa, sb);
+            break;
         default: fprintf(stderr, "whisper_mi355x: fp8 GEMM epilogue %d not supported\n", epi); abort();
     }
 }
 
 void launch_gemm_fp8(DType dt, int epi, const GemmArgs& g, const float* a_scale, const float* b_scale, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0) return;
-    if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || !a_scale || !b_scale) {
+    const bool mx_in = !a_scale && g.mx_scale && epi == EPI_RESID;
+    const bool mx_out = epi == EPI_GELU_MX;
+    if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || (!a_scale && !mx_in) || !b_scale ||
+        (mx_out && (g.N % 32 != 0 || !g.mx_scale || !a_scale)) || (mx_in && (g.a_rpb != g.M || g.a_rstride != g.K))) {
         fprintf(stderr, "whisper_mi355x: fp8 gemm shape not supported (N=%d K=%d)\n", g.N, g.K);
         abort();
     }

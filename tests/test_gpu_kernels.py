@@ -77,7 +77,7 @@ def test_gemm_resid_epilogue(wrs, ctx, M, N, K):
     pa, pb, pbias, px = _dev(wrs, ctx, A), _dev(wrs, ctx, B), _dev(wrs, ctx, bias), _dev(wrs, ctx, x0)
     ms = C.c_float()
     assert L.whisper_mi355x_debug_gemm(ctx.ptr, 2, C.c_void_p(pa), M, K, C.c_void_p(pb), N, C.c_void_p(pbias),
-                                       C.c_void_p(px), 1, C.byref(ms)) == 0
+                                       C.c_void_p(px), 0, C.byref(ms)) == 0
     out = np.empty_like(x0)
     L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(px), out.nbytes, 2)
     for p in (pa, pb, pbias, px):

@@ -3,11 +3,13 @@
 busy = SQ_VALU_MFMA_BUSY_CYCLES (MFMA pipe cycles summed over the SIMDs that ran the dispatch;
 32 per 32x32x16 bf16 MFMA, MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"); the dispatch's
 clock cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs). MFMA-busy fraction =
-busy / (cycles x 1024 SIMDs) (256 CUs x 4). Writes profiles/r01_pmc_mfma.json.
+busy / (cycles x 1024 SIMDs) (256 CUs x 4). Writes profiles/<tag>_pmc_mfma.json (tag: argv[1], default r02)
+and the same file under gpurun_out/ (which travels back from the GPU box).
 """
 import csv
 import glob
 import json
+import sys
 import os
 from collections import defaultdict
 
@@ -37,9 +39,11 @@ def main():
             b, g = busy / nb, grbm / ng
             out[f"{tag}:{k}"] = dict(launches=nb, mfma_busy_cycles=b, grbm_gui_active=g,
                                      mfma_busy_frac=b / (g / 8.0 * 1024.0))
-    path = os.path.join(ROOT, "profiles", "r01_pmc_mfma.json")
-    with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
+    path = os.path.join(ROOT, "profiles", f"{tag}_pmc_mfma.json")
+    for p in (path, os.path.join(ROOT, "gpurun_out", f"{tag}_pmc_mfma.json")):
+        with open(p, "w") as fh:
+            json.dump(out, fh, indent=1)
     for k, v in out.items():
         print(f"{v['mfma_busy_frac']:.3f} busy  n={v['launches']}  busy={v['mfma_busy_cycles']:.3e} "
               f"grbm={v['grbm_gui_active']:.3e}  {k[:110]}")

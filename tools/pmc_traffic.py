@@ -46,8 +46,9 @@ def main():
         wb = w * 1024 / max(1, nw)
         out[k] = dict(launches=max(nf, nw), fetch_bytes=fb, write_bytes=wb, traffic_bytes=fb + wb)
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
-    with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
+    for p in (path, os.path.join(ROOT, "gpurun_out", f"{tag}_pmc_traffic.json")):  # gpurun_out travels back
+        with open(p, "w") as fh:
+            json.dump(out, fh, indent=1)
     for k, v in out.items():
         print(f"{v['traffic_bytes'] / 1e6:10.2f} MB/launch  (fetch x2 {v['fetch_bytes'] / 1e6:.2f}, write "
               f"{v['write_bytes'] / 1e6:.2f})  n={v['launches']}  {k[:90]}")
