@@ -388,12 +388,16 @@ static void ensure_fp8(Context* c) {
     c->fp8_ready = true;
 }
 
-// fp8 mode, FC1 -> FC2: MX hand-off (FC1's epilogue quantizes per 32-column block, no separate
-// quantizer pass over the GELU output). WHISPER_MI355X_FP8_MX=0 restores the per-row requantization.
+// fp8 mode, FC1 -> FC2: MX hand-off (FC1's epilogue quantizes per 32-column block, FC2's block-scaled
+// MFMA takes the scales; no separate quantizer pass over the GELU output). Off by default
+// (WHISPER_MI355X_FP8_MX=1 enables it): measured slower on turbo at 256 clips (encode 743-815 vs
+// 578 ms per step) -- the MX-A FC2 kernel exceeds the 256-VGPR budget of a 2-wave/SIMD tile and
+// spills in its main loop (1091 vs 376 us per launch), and the FC1 MX epilogue costs 67 us more
+// than the bf16 GELU store it replaces; the 78 us requantization pass it removes does not cover either.
 static bool fp8_mx() {
     static const bool on = [] {
         const char* e = getenv("WHISPER_MI355X_FP8_MX");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     return on;
 }

@@ -784,6 +784,12 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ f32x4 mfma_mx8(i32x8 a, i32x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
+// A scale = byte SEL of `sp` (the opsel operand selects the byte: probed, tools/probe/mx_opsel.hip), so
+// four fragments' E8M0 scales travel in one VGPR
+template <int SEL>
+__device__ __forceinline__ f32x4 mfma_mx8s(i32x8 a, i32x8 b, f32x4 c, int sp) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, SEL, sp, 0, 127);
+}
 
 // MXA: A carries MX block scales (E8M0 per row and 32-k block, g.mx_scale [M][K/32], the output of an
 // EPI_GELU_MX launch) instead of a per-row f32 scale: each K-tile's 4 scale bytes per row are staged
@@ -795,8 +801,12 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
                                                         const float* __restrict__ sb) {
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int BM = 256, BK = 128;  // BK in fp8 elements = bytes
-    __shared__ u32x4 lds[2][(BM + 256) * 8];
-    __shared__ uint32_t lsc[2][MXA ? BM : 1];
+    // one __shared__ object only: a second one beside the LDS-DMA staging array makes hipcc wait
+    // vmcnt(0) before the first LDS read of every K-step (guide §5 "Projection GEMM" item 4(a)); the
+    // MX scales of a K-tile (256 rows x 4 bytes) sit after each buffer's A and B images
+    constexpr int SC16 = MXA ? BM / 4 : 0;  // u32x4 per buffer for the scales
+    __shared__ u32x4 lds[2][(BM + 256) * 8 + SC16];
+    auto lsc_ptr = [&](int buf) -> uint32_t* { return (uint32_t*)&lds[buf][(BM + 256) * 8]; };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
@@ -830,7 +840,7 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
         if constexpr (MXA) {
             if (lane < 32)
-                __builtin_amdgcn_global_load_lds((const void*)(sc_src + kt * 4), (lds_ptr_t)&lsc[kt & 1][wave * 32], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(sc_src + kt * 4), (lds_ptr_t)(lsc_ptr(kt & 1) + wave * 32), 4, 0, 0);
         }
     };
     auto stage_b = [&](int kt) {
@@ -848,7 +858,7 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     i32x8 a0[4], a1[4], b0[2], b1[2];
-    int s0[4] = {127, 127, 127, 127}, s1[4] = {127, 127, 127, 127};  // MXA: E8M0 per A fragment (row, 32-k block)
+    int s0 = 0, s1 = 0;  // MXA: byte i = E8M0 of A fragment i (its row, this lane's 32-k block)
     // lane l's operand registers 0-3 / 4-7 hold k = 16(l>>4) + [0, 16) / 64 + 16(l>>4) + [0, 16) of the
     // K-tile (probed on gfx950: tools/probe/mx_layout.hip), so the 16-byte chunks (l>>4) and
     // (l>>4) + 4 of the row are loaded: instruction k == memory k, and a 32-k MX block (scale lane
@@ -858,30 +868,36 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
         const u32x4 x = img[row * 8 + (c0 ^ sw)], y = img[row * 8 + ((c0 + 4) ^ sw)];
         return (i32x8){(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
     };
-    auto read_a = [&](int buf, int mq, i32x8 (&af)[4], int (&sf)[4]) {
+    auto read_a = [&](int buf, int mq, i32x8 (&af)[4], int& sp) {
+        if constexpr (MXA) sp = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int r = wm * 128 + (mq * 4 + i) * 16 + (lane & 15);
             af[i] = frag(&lds[buf][0], r);
-            if constexpr (MXA) sf[i] = (int)((lsc[buf][r] >> (8 * (lane >> 4))) & 0xFF);
+            if constexpr (MXA) sp |= (int)(((lsc_ptr(buf)[r] >> (8 * (lane >> 4))) & 0xFF) << (8 * i));
         }
     };
     auto read_b = [&](int buf, int nq, i32x8 (&bf)[2]) {
 #pragma unroll
         for (int j = 0; j < 2; j++) bf[j] = frag(&lds[buf][BM * 8], wn * 64 + (nq * 2 + j) * 16 + (lane & 15));
     };
-    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2], const int (&sf)[4]) {
+    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2], int sp) {
         asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; i++)
+        if constexpr (MXA) {
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-                if constexpr (MXA)
-                    acc[mq * 4 + i][nq * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                        af[i], bf[j], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0, sf[i], 0, 127);
-                else acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
+                acc[mq * 4 + 0][nq * 2 + j] = mfma_mx8s<0>(af[0], bf[j], acc[mq * 4 + 0][nq * 2 + j], sp);
+                acc[mq * 4 + 1][nq * 2 + j] = mfma_mx8s<1>(af[1], bf[j], acc[mq * 4 + 1][nq * 2 + j], sp);
+                acc[mq * 4 + 2][nq * 2 + j] = mfma_mx8s<2>(af[2], bf[j], acc[mq * 4 + 2][nq * 2 + j], sp);
+                acc[mq * 4 + 3][nq * 2 + j] = mfma_mx8s<3>(af[3], bf[j], acc[mq * 4 + 3][nq * 2 + j], sp);
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
+        }
         __builtin_amdgcn_s_setprio(0);
         asm volatile("s_barrier" ::: "memory");
     };
@@ -950,12 +966,17 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
             // lanes l, l^1 hold the two 16-column halves of one 32-column block of row m: every lane
             // takes part in the DPP exchange (rows past M compute on clamped data, store nothing)
             const float am = m < g.M ? (MXA ? 1.0f : sa[m]) : 0.0f;
+            float bv[16];
+            const int nbias = min(n, g.N - 16);  // N % 32 == 0: the 16 columns are in bounds
+#pragma unroll
+            for (int k = 0; k < 16; k += 4) {
+                const float4 b = g.bias ? *(const float4*)(g.bias + nbias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                bv[k] = b.x; bv[k + 1] = b.y; bv[k + 2] = b.z; bv[k + 3] = b.w;
+            }
             float amax = 0.0f;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                float x = (v[k] * am) * bs[k];
-                if (g.bias) x = x + g.bias[min(n + k, g.N - 1)];
-                v[k] = gelu_formula(x);
+                v[k] = gelu_formula((v[k] * am) * bs[k] + bv[k]);
                 amax = fmaxf(amax, fabsf(v[k]));
             }
             amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, amax), 0xB1, 0xF, 0xF, false)));
