@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 // after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
 // slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
 template <typename T, int EPI>
-__global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n) {
+__global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n, const int gm) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int BM = 256, BK = 64;
@@ -596,7 +596,16 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-    const int m0 = (wgid / tiles_n) * BM, n0 = (wgid % tiles_n) * 256;
+    // grouped tile order (gm > 0): each group of gm m-tiles walks its m-tiles fastest, so the
+    // workgroups an XCD runs at once share B (weight) tiles and a few A tiles in its L2
+    int mt = wgid / tiles_n, nt = wgid % tiles_n;
+    if (gm > 0) {
+        const int tiles_m = (g.M + BM - 1) / BM, per = gm * tiles_n, grp = wgid / per, f0 = grp * gm;
+        const int gsz = min(gm, tiles_m - f0), r = wgid - grp * per;
+        mt = f0 + r % gsz;
+        nt = r / gsz;
+    }
+    const int m0 = mt * BM, n0 = nt * 256;
     const T* A = (const T*)g.A;
     const T* B = (const T*)g.B;
     // DMA sources: half-tile h (rows h*128 .. +127) = 2 pieces of 8 rows x 128 B per wave
@@ -1301,6 +1310,16 @@ static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st
     else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
 }
 
+// big-GEMM tile order: 0 = row-major over (m-tile, n-tile) after the XCD remap; > 0 = groups of this
+// many m-tiles (WHISPER_MI355X_GEMM_GM, tuning)
+static int gemm_group_m() {
+    static const int v = [] {
+        const char* e = getenv("WHISPER_MI355X_GEMM_GM");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     const bool big256 = g_gemm_variant >= 2 ||
@@ -1309,7 +1328,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int tn = cdiv(g.N, 256);
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
-        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
+        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, gemm_group_m());
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {

@@ -19,6 +19,12 @@ static constexpr int LT = 1024;
 
 __device__ __forceinline__ float masked_logit(float x, int i, const SeqCtl& c, const VocabIds& v) {
     if (c.temperature > 0.0f) x = x / c.temperature;
+    // text tokens (every special id is >= eot): only the blank and the timestamp-pairing rules reach them
+    if (i < v.eot) {
+        if (c.last_ts && !c.penult_ts) return -INFINITY;
+        if (c.suppress_blank && c.is_initial && i == v.space) return -INFINITY;
+        return x;
+    }
     if (c.suppress_blank && c.is_initial && (i == v.eot || i == v.space)) return -INFINITY;
     if (i == v.not_) return -INFINITY;
     if (c.no_timestamps && i >= v.beg) return -INFINITY;
@@ -80,6 +86,9 @@ __device__ void block_argmax(float& v, int& idx, float* shv, int* shi) {
         if (shv[i] > v || (shv[i] == v && shi[i] < idx)) { v = shv[i]; idx = shi[i]; }
 }
 
+// Per-element exponentials use the hardware exp2 (__expf, a few ulp): the GPU's logits already differ
+// from the CPU's by ~1e-3, so libm-accurate exp buys no parity, and its ~20-instruction expansion per
+// element made the kernel VALU-bound.
 // The row is loaded once into registers (NPT values per thread, all loads issued back to back) and
 // every pass works on registers: a row re-read per pass from L2 with one load in flight per wave
 // made the kernel latency-bound (128 us per step at 128 rows). Per-thread accumulation runs over
@@ -110,10 +119,23 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
 
     extern __shared__ float s_row[];  // [NPT_LDS][LT]
     RowSlice x{s_row};
+    // the register part first, then the LDS part in batches of 12 loads in flight (a load -> LDS
+    // store pair per element would wait out one memory latency per element)
 #pragma unroll
-    for (int k = 0; k < NPT; k++) {
+    for (int k = NPT_LDS; k < NPT; k++) {
         const int i = tid + k * LT;
         x.set(k, i < n ? L[i] : -INFINITY);
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < NPT_LDS; k0 += 12) {
+        float t[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int i = tid + (k0 + k) * LT;
+            t[k] = i < n ? L[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int k = 0; k < 12; k++) x.set(k0 + k, t[k]);
     }
     float nosp_prob = 0.0f;
     if (c.want_nosp) {  // no-speech probability from the raw (unfiltered) logits
@@ -125,7 +147,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
         float sm = 0.0f;
 #pragma unroll
         for (int k = 0; k < NPT; k++)
-            if (tid + k * LT < n) sm += expf(x.get(k) - mx);
+            if (tid + k * LT < n) sm += __expf(x.get(k) - mx);
         sm = block_sum(sm, shf);
         const float lse = logf(sm) + mx;
         nosp_prob = expf(L[v.nosp] - lse);
@@ -144,7 +166,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
     float sm = 0.0f;
 #pragma unroll
     for (int k = 0; k < NPT; k++)
-        if (x.get(k) > -INFINITY) sm += expf(x.get(k) - mx);
+        if (x.get(k) > -INFINITY) sm += __expf(x.get(k) - mx);
     sm = block_sum(sm, shf);
     const float lse = logf(sm) + mx;
     // timestamp rule
@@ -163,7 +185,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
         const int i = tid + k * LT;
         if (i < v.beg) continue;
         const float lp = x.get(k) > -INFINITY ? x.get(k) - lse : -INFINITY;
-        if (lp > -INFINITY) sts += expf(lp - mts);
+        if (lp > -INFINITY) sts += __expf(lp - mts);
     }
     sts = block_sum(sts, shf);
     const float ts_logprob = sts > 0.0f ? logf(sts) + mts : -INFINITY;
@@ -178,7 +200,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
         if (i >= n) continue;
         float xv = x.get(k);
         if (mask_text && i < v.beg) xv = -INFINITY;
-        const float p = xv == -INFINITY ? 0.0f : expf(xv - lse);
+        const float p = xv == -INFINITY ? 0.0f : __expf(xv - lse);
         if (c.want_probs) {  // [seq][2][V]: probs, logprobs (host sampling at t > 0)
             probs[(long)s * 2 * n + i] = p;
             probs[(long)s * 2 * n + n + i] = xv == -INFINITY ? -INFINITY : xv - lse;
