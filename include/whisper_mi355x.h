@@ -88,9 +88,9 @@ WHISPER_API int whisper_mi355x_get_encoder_out(struct whisper_state * state, flo
 /* Live per-kernel-class timing with HIP events on the state's stream (used by bench.py for the
  * roofline). Classes: 0 encoder-side GEMM (work = FLOPs), 1 encoder attention (FLOPs),
  * 2 decoder cross-attention (HBM bytes), 3 decoder self-attention (bytes), 4 decoder GEMM (bytes),
- * 5 logits processing (bytes), 6 mel (bytes). class_mask bit k times class k (0 = off); every call
- * resets the counters; stats out =
- * {total ms, launches, total work}. */
+ * 5 logits processing (bytes), 6 mel (bytes). class_mask bit k times class k (0 = off); bits 8..15,
+ * when > 1, time the decoder's per-layer attention launches (classes 2, 3) of every k-th layer only.
+ * Every call resets the counters; stats out = {total ms, launches, total work}. */
 WHISPER_API int whisper_mi355x_kernel_timing(struct whisper_state * state, int class_mask);
 WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cls, double out[3]);
 
