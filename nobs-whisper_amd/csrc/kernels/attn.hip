@@ -356,7 +356,8 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
 #pragma unroll
         for (int e = 0; e < 8; e++) qv[e] = (float)qe[e];
     }
-    // phase 1: scores; U key rows in flight per lane group before the first use
+    // phase 1: scores; U key rows in flight per lane group before the first use (U = 16 measured no
+    // faster at 16 clips)
     constexpr int U = 8;
     const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
