@@ -26,6 +26,7 @@ rng = np.random.default_rng(0)
 REPS = 200
 Ms = [int(x) for x in os.environ.get("DEC_M", "16,128").split(",")]
 splits_list = [int(x) for x in os.environ.get("DEC_SPLITS", "0").split(",")]
+variants = [int(x) for x in os.environ.get("DEC_VARIANTS", "1").split(",")]  # 1 = split-K + reduce (the decode path)
 for M in Ms:
     for (N, K, name, epi) in [(3 * d, d, "qkv", 0), (d, d, "q", 0), (4 * d, d, "fc1", 1), (d, d, "out+ln", -1),
                               (d, 4 * d, "fc2+ln", -1), (51866, d, "logits", 4)]:
@@ -35,7 +36,7 @@ for M in Ms:
         out = np.zeros((M, N), np.float32)
         ln = np.ones(N, np.float32)
         ptrs = [_dev(wrs, ctx, a) for a in (A, B, bias, out, ln, ln, out)]
-        for v in (1,):
+        for v in variants:
             for sp in splits_list:
                 L.whisper_mi355x_set_gemm_variant(v)
                 L.whisper_mi355x_set_dec_splits(sp)
