@@ -109,6 +109,12 @@ WHISPER_API int whisper_mi355x_debug_gemm_fp8(struct whisper_context * ctx, int 
                                               const float * a_scale, int M, int K, const void * B8,
                                               const float * b_scale, int N, const float * bias, void * out,
                                               int reps, float * ms);
+// decode-step GEMM with e4m3 weights (fp8 mode decoder): out = A[M][K] (compute dtype) .
+// (B8[N][K] e4m3 * b_scale[n])^T + bias, epilogue `epi`, M <= 128, K % 64 == 0; with epi 2 and
+// ln_w != null the fused residual + LayerNorm form (x = out in/out, y = LN output)
+WHISPER_API int whisper_mi355x_debug_gemm_w8(struct whisper_context * ctx, int epi, const void * A, int M, int K,
+                                             const void * B8, const float * b_scale, int N, const float * bias,
+                                             void * out, const float * ln_w, const float * ln_b, void * y);
 // MX hand-off of the fp8 encoder: epi 8 (EPI_GELU_MX) writes out = e4m3 bytes [M][N] of GELU(C) with one
 // E8M0 scale per row and 32-column block into mx_scale [M][N/32]; epi 2 (EPI_RESID) with a_scale = NULL
 // reads A as MX e4m3 with those block scales (out f32 [M][N] += C). Device pointers.

@@ -546,6 +546,28 @@ int whisper_mi355x_debug_gemm_fp8(struct whisper_context* ctx, int epi, const vo
     hipStreamDestroy(st);
     return 0;
 }
+int whisper_mi355x_debug_gemm_w8(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B8,
+                                 const float* b_scale, int N, const float* bias, void* out, const float* ln_w,
+                                 const float* ln_b, void* y) {
+    if (!ctx || !b_scale || M < 1 || M > 128 || K % 64) return -1;
+    hipSetDevice(ctx->c.device);
+    GemmArgs g{};
+    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+    g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
+    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+    g.w8_scale = b_scale;
+    if (epi == EPI_RESID) {
+        if (!ln_w || !y) return -1;
+        g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
+    }
+    g.splitk_ws_elems = 16L * M * N;
+    WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+    launch_gemm(ctx->c.dt, epi, g, nullptr);
+    WM_CHECK(hipDeviceSynchronize());
+    hipFree(g.splitk_ws);
+    return 0;
+}
 int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale,
                                      void* mx_scale, int M, int K, const void* B8, const float* b_scale, int N,
                                      const float* bias, void* out) {

@@ -66,6 +66,7 @@ struct KT {
 static void drop_graphs(whisper_state* s) {
     for (auto& g : s->dec_graphs) {
         hipGraphExecDestroy(g.exec);
+        if (g.exec2) hipGraphExecDestroy(g.exec2);
         for (auto& e : g.ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     }
     s->dec_graphs.clear();
@@ -360,16 +361,29 @@ static GemmArgs gemm_plain(const void* A, int M, int K, const void* B, int N, co
     return g;
 }
 
+// fp8 mode, decoder half: WHISPER_MI355X_FP8_DEC=1 (read when a context first quantizes its weights).
+// Off by default: correct (tests/test_gpu_fp8.py) but slower, because the decode-step GEMMs are
+// latency-bound, not bound by their weight bytes (profiles/r02_fp8_decoder_ab.txt: large-v3 fp8 at
+// 128 clips decode 849 -> 936 ms per step, turbo fp8 at 256 clips 193 -> 210 ms).
+static bool dec_fp8() {
+    const char* e = getenv("WHISPER_MI355X_FP8_DEC");
+    return e && atoi(e) == 1;
+}
+
 // fp8 encoder weights: e4m3 copies of QKV, FC1 and FC2 with per-output-row scales, quantized on the
-// device from the bf16 weights once per context (after load or the RCCL weight broadcast).
+// device from the bf16 weights once per context (after load or the RCCL weight broadcast); in the
+// same arena the decoder's decode-step projections (dec_fp8()).
 static void ensure_fp8(Context* c) {
     std::lock_guard<std::mutex> lk(c->fp8_mu);
     if (c->fp8_ready) return;
     const Hparams& hp = c->hp;
     const size_t d = hp.n_audio_state, nl = hp.n_audio_layer;
     const size_t per = 3 * d * d + 4 * d * d + 4 * d * d, per_s = (3 * d + 4 * d + d) * sizeof(float);
+    // decoder: wqkv [3t][t], wo / wxq / wxo [t][t], w1 [4t][t], w2 [t][4t] (+ one f32 scale per row)
+    const size_t t = hp.n_text_state, nd = dec_fp8() ? hp.n_text_layer : 0;
+    const size_t per_d = 14 * t * t, per_ds = (3 * t + 3 * t + 4 * t + t) * sizeof(float);
     WM_CHECK(hipSetDevice(c->device));
-    WM_CHECK(hipMalloc((void**)&c->arena8, nl * (per + per_s)));
+    WM_CHECK(hipMalloc((void**)&c->arena8, nl * (per + per_s) + nd * (per_d + per_ds)));
     c->enc8.assign(nl, Context::Fp8Layer{});
     char* p = c->arena8;
     for (size_t l = 0; l < nl; l++) {
@@ -384,6 +398,22 @@ static void ensure_fp8(Context* c) {
         launch_quant_rows_fp8(c->dt, L.wqkv, 3 * d, (int)d, f.wqkv, f.sqkv, nullptr);
         launch_quant_rows_fp8(c->dt, L.w1, 4 * d, (int)d, f.w1, f.s1, nullptr);
         launch_quant_rows_fp8(c->dt, L.w2, d, (int)(4 * d), f.w2, f.s2, nullptr);
+    }
+    c->dec8.assign(nd, Context::Fp8Dec{});
+    for (size_t l = 0; l < nd; l++) {
+        Context::Fp8Dec& f = c->dec8[l];
+        const LayerW& L = c->w.dec[l];
+        auto q = [&](const void* w, size_t rows, size_t cols, void*& q8, float*& sc) {
+            q8 = p; p += rows * cols;
+            sc = (float*)p; p += rows * sizeof(float);
+            launch_quant_rows_fp8(c->dt, w, (long)rows, (int)cols, q8, sc, nullptr);
+        };
+        q(L.wqkv, 3 * t, t, f.wqkv, f.sqkv);
+        q(L.wo, t, t, f.wo, f.so);
+        q(L.wxq, t, t, f.wxq, f.sxq);
+        q(L.wxo, t, t, f.wxo, f.sxo);
+        q(L.w1, 4 * t, t, f.w1, f.s1);
+        q(L.w2, t, 4 * t, f.w2, f.s2);
     }
     WM_CHECK(hipDeviceSynchronize());
     c->fp8_ready = true;
@@ -576,8 +606,15 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     void* dff = (char*)w.dff + (size_t)v.r0 * 4 * d * E;
     void* qx = w.qx ? (void*)((char*)w.qx + (size_t)v.r0 * 2 * H * d * E) : nullptr;
     auto gemm = [&](int cls, int epi, const GemmArgs& g) { tgemm_ws(s, cls, dt, epi, g, st, v.splitk, v.splitk_elems); };
-    auto resid = [&](const void* A, int K, const void* Wt, const float* bias, const float* lnw, const float* lnb) {
-        GemmArgs g = gemm_plain(A, n_tok, K, Wt, d, bias, dx, d);
+    // fp8 mode: decode steps read the e4m3 copies of the layer's projection weights
+    const bool w8 = fused && c->fp8_enc && !c->dec8.empty();
+    auto use8 = [&](GemmArgs g, void* q8, float* sc) {
+        if (w8) { g.B = q8; g.w8_scale = sc; }
+        return g;
+    };
+    auto resid = [&](const void* A, int K, const void* Wt, const float* bias, const float* lnw, const float* lnb,
+                     void* q8 = nullptr, float* sc = nullptr) {
+        GemmArgs g = use8(gemm_plain(A, n_tok, K, Wt, d, bias, dx, d), q8, sc);
         if (fused) { g.ln_w = lnw; g.ln_b = lnb; g.ln_out = dh; }
         gemm(KCLS, EPI_RESID, g);
         if (!fused && lnw) launch_layernorm(dt, dx, nullptr, n_tok, d, lnw, lnb, dh, st);
@@ -589,8 +626,9 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     }
     // decode steps: the QKV (and, cache mode, cross-Q) projections leave split-K partial sums that
     // the attention kernels reduce in their prologue (no separate reduce launch)
-    auto partials = [&](const void* A, const void* Wt, int N, const float* bias, float scale) -> DecSlabs {
-        GemmArgs g = gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N);
+    auto partials = [&](const void* A, const void* Wt, int N, const float* bias, float scale, void* q8,
+                        float* sc) -> DecSlabs {
+        GemmArgs g = use8(gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N), q8, sc);
         g.splitk_ws = v.splitk;
         g.splitk_ws_elems = v.splitk_elems;
         KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
@@ -603,9 +641,11 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
+        static const Context::Fp8Dec no8{};
+        const Context::Fp8Dec& F = w8 ? c->dec8[l] : no8;
         const bool kt_layer = l % kt_stride == 0;
         if (fused) {
-            const DecSlabs sl = partials(dh, Lw.wqkv, 3 * d, Lw.bqkv, c->k_scale);
+            const DecSlabs sl = partials(dh, Lw.wqkv, 3 * d, Lw.bqkv, c->k_scale, F.wqkv, F.sqkv);
             KT kt(s, K_ATTN_SELF, self_share, st, kt_layer);
             launch_attn_self_step(dt, sl, w.self, slot, pos, n_tok, L, l, H, hp.n_text_ctx, d, datt, st);
         } else {
@@ -617,11 +657,11 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             KT kt(s, K_ATTN_SELF, self_share, st, kt_layer);
             launch_attn_prefill(dt, dq, d, w.self, slot, nkv_self, w.qtiles, w.n_qtiles, L, l, H, hp.n_text_ctx, d, datt, st);
         }
-        resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b);
+        resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b, F.wo, F.so);
         if (xdirect) {
             // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
             // -> one pass over E per clip -> split merge + Wv
-            GemmArgs g = gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d);
+            GemmArgs g = use8(gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d), F.wxq, F.sxq);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
             gemm(KCLS, EPI_STORE, g);
             const int Ta = hp.n_audio_ctx, S = xattn_splits(n_tok, Ta);
@@ -640,7 +680,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
                                      W.bkv_cross + (size_t)(2 * l + 1) * d, n_tok, d, H, datt, st);
             }
         } else if (fused) {
-            const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale);
+            const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);
             KT kt(s, K_ATTN_CROSS, (double)n_tok * hp.n_audio_ctx * kvrow, st, kt_layer);  // decode steps only
             launch_attn_cross_step(dt, sl, w.cross, slot, nkv_cross, n_tok, L, l, H, hp.n_audio_ctx, d, datt, st);
         } else {
@@ -650,10 +690,10 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             KT kt(s, K_OTHER, (double)n_tok * hp.n_audio_ctx * kvrow, st);
             launch_attn_prefill(dt, dq, d, w.cross, slot, nkv_cross, w.qtiles, w.n_qtiles, L, l, H, hp.n_audio_ctx, d, datt, st);
         }
-        resid(datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b);
-        gemm(KCLS, EPI_GELU, gemm_plain(dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d));
-        if (l + 1 < L) resid(dff, 4 * d, Lw.w2, Lw.b2, W.dec[l + 1].ln1_w, W.dec[l + 1].ln1_b);
-        else if (fused) resid(dff, 4 * d, Lw.w2, Lw.b2, W.lnd_w, W.lnd_b);  // dh = final LN of every row
+        resid(datt, d, Lw.wxo, Lw.bxo, Lw.ln2_w, Lw.ln2_b, F.wxo, F.sxo);
+        gemm(KCLS, EPI_GELU, use8(gemm_plain(dh, n_tok, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d), F.w1, F.s1));
+        if (l + 1 < L) resid(dff, 4 * d, Lw.w2, Lw.b2, W.dec[l + 1].ln1_w, W.dec[l + 1].ln1_b, F.w2, F.s2);
+        else if (fused) resid(dff, 4 * d, Lw.w2, Lw.b2, W.lnd_w, W.lnd_b, F.w2, F.s2);  // dh = final LN of every row
         else resid(dff, 4 * d, Lw.w2, Lw.b2, nullptr, nullptr);
     }
     if (fused) {
@@ -669,12 +709,39 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
 // hipGraph), so that each group's chain of small latency-bound launches could overlap the other's.
 // Off by default: measured slower on large-v3 at 128 clips (2360-2392 vs 2729-2740 audio-s/s;
 // the cross-attention pass at 64 clips per group reads E at 3.6 instead of 4.7 TB/s).
+// Above 128 clips a step does not fit one fused pass (<= 128 rows), so it runs as two fused groups
+// by default (measured the same as the unfused path in bf16: decode 213 vs 217 ms per step on turbo
+// at 256 clips; the fp8 decoder weights exist only on the fused path).
 static int dec_groups(int n_tok) {
     static const int g = [] {
         const char* e = getenv("WHISPER_MI355X_DEC_STREAMS");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
+    if (g == 0) return n_tok > 128 && n_tok <= 256 ? 2 : 1;
     return (g >= 2 && n_tok >= 32) ? 2 : 1;
+}
+
+// the two row groups of a decode step: rows [0, na) on the state's stream, [na, n) on stream2, each
+// with its own half of the split-K slabs and its own cross-attention partials
+static void dec_views(Context* c, whisper_state* s, int n_tok, bool xdirect, DecView& a, DecView& b) {
+    Workspace& w = s->ws;
+    const int H = c->hp.n_text_head, d = c->hp.n_text_state;
+    const int na = (n_tok + 1) / 2, nb = n_tok - na;
+    const long half = w.splitk_elems / 2;
+    const long xoff = xdirect ? (long)na * xattn_splits(na, c->hp.n_audio_ctx) : 0;
+    a = DecView{0, na, s->stream, w.splitk, half, w.xo, w.xml};
+    b = DecView{na, nb, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
+                w.xml ? w.xml + xoff * H * 2 : nullptr};
+}
+
+// WHISPER_MI355X_DEC_GRAPHS2=1: the two row groups as two separate hipGraphs launched on two streams
+// (two hardware queues), instead of two branches of one graph
+static bool dec_two_graphs() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_DEC_GRAPHS2");
+        return e && atoi(e) == 1;
+    }();
+    return on;
 }
 
 static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
@@ -686,13 +753,9 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
         decoder_rows(c, s, v, n_rows, fused, xdirect, 1.0);
         return;
     }
-    const int H = c->hp.n_text_head, d = c->hp.n_text_state;
-    const int na = (n_tok + 1) / 2, nb = n_tok - na;
-    const long half = w.splitk_elems / 2;
-    const long xoff = xdirect ? (long)na * xattn_splits(na, c->hp.n_audio_ctx) : 0;
-    const DecView a{0, na, s->stream, w.splitk, half, w.xo, w.xml};
-    const DecView b{na, nb, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
-                    w.xml ? w.xml + xoff * H * 2 : nullptr};
+    DecView a, b;
+    dec_views(c, s, n_tok, xdirect, a, b);
+    const int na = a.n, nb = b.n;
     WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
     WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
     decoder_rows(c, s, a, na, true, xdirect, (double)na / n_tok);
@@ -1058,6 +1121,37 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     whisper_state::DecGraph* G = nullptr;
     for (auto& g : s->dec_graphs)
         if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct) G = &g;
+    if (dec_two_graphs() && dec_groups(n) == 2 && cdiv(n, 2) <= 128 && s->ktime_mask == 0) {
+        // two graphs, one per row group and stream: both wait for the token upload, the logits kernel
+        // waits for both
+        DecView a, b;
+        dec_views(c, s, n, s->direct, a, b);
+        if (!G) {
+            whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, nullptr, {}};
+            hipGraph_t graph;
+            WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+            decoder_rows(c, s, a, a.n, true, s->direct, (double)a.n / n);
+            WM_CHECK(hipStreamEndCapture(s->stream, &graph));
+            WM_CHECK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+            WM_CHECK(hipGraphDestroy(graph));
+            WM_CHECK(hipStreamBeginCapture(s->stream2, hipStreamCaptureModeThreadLocal));
+            decoder_rows(c, s, b, b.n, true, s->direct, (double)b.n / n);
+            WM_CHECK(hipStreamEndCapture(s->stream2, &graph));
+            WM_CHECK(hipGraphInstantiate(&g.exec2, graph, nullptr, nullptr, 0));
+            WM_CHECK(hipGraphDestroy(graph));
+            s->dec_graphs.push_back(std::move(g));
+            G = &s->dec_graphs.back();
+        }
+        WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
+        WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
+        WM_CHECK(hipGraphLaunch(G->exec2, s->stream2));
+        WM_CHECK(hipGraphLaunch(G->exec, s->stream));
+        WM_CHECK(hipEventRecord(s->ev_join, s->stream2));
+        WM_CHECK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
+        logits_launch(c, s, n);
+        logits_finish(S, n, any, probs_rows);
+        return;
+    }
     if (!G) {
         whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, nullptr, {}};
         hipGraph_t graph;

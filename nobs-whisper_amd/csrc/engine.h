@@ -92,6 +92,11 @@ struct Context {
     std::mutex fp8_mu;
     std::vector<Fp8Layer> enc8;
     char* arena8 = nullptr;
+    // fp8 mode, decoder: the decode-step projections (self QKV, self out, cross Q, cross out, FC1, FC2)
+    // read e4m3 weights with per-output-row scales (same quantizer, same arena); the token embedding
+    // (logits), the cross-attention K/V weights and prefill keep the compute type
+    struct Fp8Dec { void *wqkv, *wo, *wxq, *wxo, *w1, *w2; float *sqkv, *so, *sxq, *sxo, *s1, *s2; };
+    std::vector<Fp8Dec> dec8;
 };
 
 struct TokenData {
@@ -189,7 +194,7 @@ struct whisper_state {
     std::vector<KPending> kpending;
     std::vector<hipEvent_t> kpool;
     // decode steps replayed as hipGraphs (one per active-sequence count and timing mask)
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; hipGraphExec_t exec; std::vector<KPending> ev; };
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; hipGraphExec_t exec; std::vector<KPending> ev; hipGraphExec_t exec2 = nullptr; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step

@@ -65,6 +65,8 @@ struct GemmArgs {
     // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
     // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
     uint8_t* mx_scale;
+    // decode-step GEMMs in fp8 mode: B is OCP e4m3 [N][K] bytes, column n scaled by w8_scale[n]
+    const float* w8_scale;
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);

@@ -1065,12 +1065,18 @@ __global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const T* __restrict
 // one memory latency per four K-tiles. The grid is (N/64) x splits with the partial tile written
 // to the split-K slab (or through the epilogue when the chunk is the whole K). Rows past M are
 // clamped (their outputs are never stored).
-template <typename T, int EPI, bool SPLIT, int AUXB = 0>
+// W8 (fp8 mode, g.w8_scale != null): the weights are OCP e4m3 bytes [N][K] with one f32 scale per
+// output column; a B tile is 64 rows x 64 bytes (4 chunks of 16 bytes per row, chunk index XOR
+// (row>>2)&3), each lane's 8 bytes are widened to the MFMA type in registers (exact: e4m3 values are
+// representable in f16 and bf16) and the column scale multiplies the f32 sum before the store. Half
+// the weight bytes of the decode step; the activations stay in the compute type.
+template <typename T, int EPI, bool SPLIT, int AUXB = 0, bool W8 = false>
 __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const int kc) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int BM = 128, BN = 64, BK = 64, MAXT = 4;
-    constexpr int STAGE = (BM + BN) * 8;  // u32x4 per stage
+    constexpr int BCH = W8 ? 4 : 8;             // 16-byte chunks per B row
+    constexpr int STAGE = BM * 8 + BN * BCH;    // u32x4 per stage
     __shared__ u32x4 lds[MAXT * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each 64 rows x 32 columns
@@ -1082,6 +1088,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
     // per stage: A = 16 pieces of 8 rows (4 per wave), B = 8 pieces (2 per wave)
     const T* a_src[4];
     const T* b_src[2];
+    const uint8_t* b8_src = nullptr;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int r = (wave * 4 + i) * 8 + (lane >> 3);
@@ -1089,22 +1096,34 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         const int m = min(r, g.M - 1);
         a_src[i] = A + (long)m * g.a_rstride + k0 + c * 8;
     }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const int r = (wave * 2 + i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
+    if constexpr (W8) {  // one piece per wave: 16 rows x 4 chunks; LDS slot p = row*4 + phys chunk
+        const int r = wave * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((r >> 2) & 3);
         const int n = min(n0 + r, g.N - 1);
-        b_src[i] = B + (long)n * g.K + k0 + c * 8;
+        b8_src = (const uint8_t*)g.B + (long)n * g.K + k0 + c * 16;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int r = (wave * 2 + i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const int n = min(n0 + r, g.N - 1);
+            b_src[i] = B + (long)n * g.K + k0 + c * 8;
+        }
     }
     auto issue = [&](int t) {
         u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
         for (int i = 0; i < 4; i++)
             __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&st[(wave * 4 + i) * 64], 16, 0, 0);
+        if constexpr (W8) {
+            __builtin_amdgcn_global_load_lds((const void*)(b8_src + t * BK), (lds_ptr_t)&st[BM * 8 + wave * 64], 16, 0, AUXB);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 2; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, AUXB);
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, AUXB);
+        }
     };
+    constexpr int PER_STAGE = W8 ? 5 : 6;  // DMA instructions per wave and stage
     for (int t = 0; t < min(nkt, MAXT); t++) issue(t);
     f32x4 acc[4][2];
 #pragma unroll
@@ -1112,12 +1131,19 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < nkt; t++) {
-        // this wave's DMAs of stage t have landed when at most 6 per later issued stage are outstanding
+        // this wave's DMAs of stage t have landed when at most PER_STAGE per later issued stage are outstanding
         const int ahead = min(nkt - 1, t + MAXT - 1) - t;
-        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
-        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (PER_STAGE == 6) {
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
         const u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -1131,7 +1157,28 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const int row = wn * 32 + j * 16 + (lane & 15);
-                bfr[j] = __builtin_bit_cast(FT, st[BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+                if constexpr (W8) {
+                    // 8 e4m3 bytes: 16-byte chunk ch>>1 (swizzled), half ch&1
+                    const uint2 w8 = ((const uint2*)&st[BM * 8 + row * 4 + ((ch >> 1) ^ ((row >> 2) & 3))])[ch & 1];
+                    // v_cvt_scalef32_pk_{bf16,f16}_fp8: two bytes -> two values per instruction (scale 1)
+                    uint32_t e[4];
+                    if constexpr (std::is_same<T, half_t>::value) {
+                        typedef _Float16 v2h __attribute__((ext_vector_type(2)));
+                        e[0] = __builtin_bit_cast(uint32_t, (v2h)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w8.x, 1.0f, false));
+                        e[1] = __builtin_bit_cast(uint32_t, (v2h)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w8.x, 1.0f, true));
+                        e[2] = __builtin_bit_cast(uint32_t, (v2h)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w8.y, 1.0f, false));
+                        e[3] = __builtin_bit_cast(uint32_t, (v2h)__builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w8.y, 1.0f, true));
+                    } else {
+                        typedef __bf16 v2b __attribute__((ext_vector_type(2)));
+                        e[0] = __builtin_bit_cast(uint32_t, (v2b)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w8.x, 1.0f, false));
+                        e[1] = __builtin_bit_cast(uint32_t, (v2b)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w8.x, 1.0f, true));
+                        e[2] = __builtin_bit_cast(uint32_t, (v2b)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w8.y, 1.0f, false));
+                        e[3] = __builtin_bit_cast(uint32_t, (v2b)__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w8.y, 1.0f, true));
+                    }
+                    bfr[j] = __builtin_bit_cast(FT, e);
+                } else {
+                    bfr[j] = __builtin_bit_cast(FT, st[BM * 8 + row * 8 + (ch ^ ((row >> 1) & 7))]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 4; i++)
@@ -1149,12 +1196,14 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         for (int j = 0; j < 2; j++) {
             const int n = n0 + wn * 32 + j * 16 + (lane & 15);
             if (n >= g.N) continue;
+            const float wsc = W8 ? g.w8_scale[n] : 1.0f;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
                 if (m >= g.M) continue;
-                if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
-                else epilogue<EPI, T>(g, m, n, acc[i][j][r]);
+                const float v = W8 ? acc[i][j][r] * wsc : acc[i][j][r];
+                if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = v;
+                else epilogue<EPI, T>(g, m, n, v);
             }
         }
 }
@@ -1322,6 +1371,13 @@ static int gemm_group_m() {
 
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
+    if (g.w8_scale) {  // e4m3 weights: the decode-step split-K kernel only
+        const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
+        if (!(g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0 && (EPI != EPI_RESID || fused_ln))) {
+            fprintf(stderr, "whisper_mi355x: e4m3 weights need the decode-step GEMM path (M %d <= 128, K %% 64 == 0)\n", g.M);
+            abort();
+        }
+    }
     const bool big256 = g_gemm_variant >= 2 ||
                         (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && big256) {
@@ -1354,16 +1410,22 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
-        const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64;
+        const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64 && !g.w8_scale;
+        if (g.w8_scale && (long)splits * g.M * g.N > g.splitk_ws_elems) {
+            fprintf(stderr, "whisper_mi355x: e4m3 decode GEMM: split-K workspace too small\n");
+            abort();
+        }
         if ((long)splits * g.M * g.N <= g.splitk_ws_elems && !small_unsplit) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
-                if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<tiles, 256, 0, st>>>(g, kc);
+                if (g.w8_scale) gemm_dec_kernel<T, EPI, false, 2, true><<<tiles, 256, 0, st>>>(g, kc);
+                else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<tiles, 256, 0, st>>>(g, kc);
                 else gemm_dec_kernel<T, EPI, false><<<tiles, 256, 0, st>>>(g, kc);
                 return;
             }
-            if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            if (g.w8_scale) gemm_dec_kernel<T, EPI, true, 2, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
             else gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
@@ -1445,7 +1507,8 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     const int kc = cdiv(nk, splits) * 64;
     splits = cdiv(g.K, kc);
     if ((long)splits * g.M * g.N > g.splitk_ws_elems) return 0;
-    if (dec_weight_nt()) gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    if (g.w8_scale) gemm_dec_kernel<T, EPI_STORE, true, 2, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    else if (dec_weight_nt()) gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
     else gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
     return splits;
 }

@@ -27,10 +27,11 @@ for n in [int(x) for x in os.environ.get("NS", "128,64").split(",")]:
         L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(p), a.ctypes.data, a.nbytes, 1)
         ptrs.append(p)
     po = L.whisper_mi355x_dev_alloc(ctx.ptr, n * d * 2)
-    ms = C.c_float()
-    assert L.whisper_mi355x_debug_xattn(ctx.ptr, *[C.c_void_p(p) for p in ptrs], n, Tn, d, 64 ** -0.25, 0, 8.0, C.c_void_p(po),
-                                        20, C.byref(ms)) == 0
-    print(f"n={n} d={d} {ms.value * 1e3:.1f} us per call "
-          f"(qproj+step+combine), E {n * Tn * d * 2 / (ms.value * 1e-3) / 1e9:.0f} GB/s (whole call)", flush=True)
+    for sp in [int(x) for x in os.environ.get("SPLITS", "0").split(",")]:  # 0 = the engine's choice
+        ms = C.c_float()
+        assert L.whisper_mi355x_debug_xattn(ctx.ptr, *[C.c_void_p(p) for p in ptrs], n, Tn, d, 64 ** -0.25, sp, 8.0,
+                                            C.c_void_p(po), 20, C.byref(ms)) == 0
+        print(f"n={n} d={d} splits={sp} {ms.value * 1e3:.1f} us per call "
+              f"(qproj+step+combine), E {n * Tn * d * 2 / (ms.value * 1e-3) / 1e9:.0f} GB/s (whole call)", flush=True)
     for p in ptrs + [po]:
         L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
