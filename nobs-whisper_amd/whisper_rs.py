@@ -12,7 +12,7 @@ import os
 from dataclasses import dataclass
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libwhisper_mi355x.so")
+LIB_PATH = os.environ.get("WHISPER_MI355X_LIB") or os.path.join(HERE, "lib", "libwhisper_mi355x.so")  # override: A/B of two builds
 ENGINE_LIB_PATH = os.path.join(HERE, "lib", "libnobs_whisper_engine.so")
 
 # The app's default custom vocabulary (src-tauri/src/config.rs:40-42): the initial prompt of every
