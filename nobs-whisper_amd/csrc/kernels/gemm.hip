@@ -1336,6 +1336,23 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
 
 int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
 static int dec_splits_override() { return g_dec_splits; }
+// decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU; default), or
+// with WHISPER_MI355X_DEC_FILL=0 the smallest reaching >= 160; both with chunks of >= 2 K-tiles and
+// <= 8 splits. Large-v3: FC1 2 -> 3 splits, QKV 3 -> 4, the N = d GEMMs unchanged at 7-8; decode
+// 844 -> 838 ms per step at 128 clips, 659 -> 654 at 64 (profiles/r02_dec_fill_ab.txt).
+static int dec_splits_for(int tiles, int nk) {
+    static const bool fill = [] {
+        const char* e = getenv("WHISPER_MI355X_DEC_FILL");
+        return !(e && atoi(e) == 0);
+    }();
+    int splits = 1;
+    if (fill) {
+        while (tiles * (splits + 1) <= 256 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+    } else {
+        while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+    }
+    return splits;
+}
 // decode-step weights are read once per step by one workgroup each: non-temporal LDS-DMA (aux = 2;
 // 3058-3070 vs 3053-3059 audio-s/s). WHISPER_MI355X_DEC_NT=0 restores the default policy (A/B).
 static bool dec_weight_nt() {
@@ -1405,8 +1422,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         // K-tiles measured faster in isolation, 9.6 vs 10.4 us at N = K = 1280, but not in the
         // decode step: 82.0 vs 81.6 us of GEMM + reduce per layer.)
         const int tiles = cdiv(g.N, 64);
-        int splits = 1;
-        while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+        int splits = dec_splits_for(tiles, nk);
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
@@ -1501,8 +1517,7 @@ template <typename T>
 static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     if (!g.splitk_ws || g.M > 128 || g.K % 64 != 0) return 0;
     const int nk = g.K / 64, tiles = cdiv(g.N, 64);
-    int splits = 1;
-    while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+    int splits = dec_splits_for(tiles, nk);
     if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
     const int kc = cdiv(nk, splits) * 64;
     splits = cdiv(g.K, kc);
