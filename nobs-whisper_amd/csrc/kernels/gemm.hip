@@ -1338,16 +1338,22 @@ int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (
 static int dec_splits_override() { return g_dec_splits; }
 // decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU; default), or
 // with WHISPER_MI355X_DEC_FILL=0 the smallest reaching >= 160; both with chunks of >= 2 K-tiles and
-// <= 8 splits. Large-v3: FC1 2 -> 3 splits, QKV 3 -> 4, the N = d GEMMs unchanged at 7-8; decode
-// 844 -> 838 ms per step at 128 clips, 659 -> 654 at 64 (profiles/r02_dec_fill_ab.txt).
+// at most WHISPER_MI355X_DEC_MAXS (12) splits. Independent of M, so a row's sums never depend on the
+// batch. Large-v3: FC1 2 -> 3 splits, QKV 3 -> 4, N = d GEMMs 7 -> 10, FC2 8 -> 12; decode 844 -> 838
+// ms per step at 128 clips, 659 -> 654 at 64, 433 -> 413 at 16 (profiles/r02_dec_fill_ab.txt; the
+// 12-split cap alone: 837 -> 839 at 128 clips, 422 -> 413 at 16).
 static int dec_splits_for(int tiles, int nk) {
     static const bool fill = [] {
         const char* e = getenv("WHISPER_MI355X_DEC_FILL");
         return !(e && atoi(e) == 0);
     }();
+    static const int maxs = [] {
+        const char* e = getenv("WHISPER_MI355X_DEC_MAXS");
+        return e ? std::max(1, std::min(16, atoi(e))) : 12;
+    }();
     int splits = 1;
     if (fill) {
-        while (tiles * (splits + 1) <= 256 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
+        while (tiles * (splits + 1) <= 256 && splits < maxs && (splits + 1) * 2 <= nk) splits++;
     } else {
         while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
     }
