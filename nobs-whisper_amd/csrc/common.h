@@ -67,6 +67,7 @@ __device__ __forceinline__ double block256_sum_d(double x, double* sh) {
 template <typename T, int NPT>
 __device__ __forceinline__ void block256_layernorm(float (&v)[NPT], int D, const float* __restrict__ w,
                                                    const float* __restrict__ b, T* __restrict__ y, double* sh) {
+#pragma clang fp contract(off)  // (v*scale)*w + b separately rounded, as ggml_norm (the __f*_rn forms alone get fused)
     const int tid = threadIdx.x;
     double s = 0.0;
 #pragma unroll
@@ -87,7 +88,7 @@ __device__ __forceinline__ void block256_layernorm(float (&v)[NPT], int D, const
 #pragma unroll
     for (int k = 0; k < NPT; k++) {
         const int n = tid + 256 * k;
-        if (n < D) y[n] = (T)__fadd_rn(__fmul_rn(__fmul_rn(v[k], scale), w[n]), b[n]);
+        if (n < D) y[n] = (T)((v[k] * scale) * w[n] + b[n]);  // plain ops: the pragma applies
     }
 }
 

@@ -1280,6 +1280,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_resid_ln_kernel(const GemmA
 // consecutive columns (16-byte slab reads, all splits in flight at once), ceil(N/256) waves per row.
 template <typename T>
 __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const GemmArgs g, int splits) {
+#pragma clang fp contract(off)  // ggml_norm's separately rounded ops (the __f*_rn forms alone are contracted)
     __shared__ double sh[16];
     const int m = blockIdx.x, tid = threadIdx.x, nw = blockDim.x >> 6;
     const long total = (long)g.M * g.N;
@@ -1330,7 +1331,7 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
     const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
     T y[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) y[k] = (T)__fadd_rn(__fmul_rn(__fmul_rn(x[k], scale), wv[k]), bv[k]);
+    for (int k = 0; k < 4; k++) y[k] = (T)((x[k] * scale) * wv[k] + bv[k]);  // plain ops: the pragma applies
     *(uint2*)((T*)g.ln_out + (long)m * g.N + n) = *(const uint2*)y;
 }
 
