@@ -1361,7 +1361,10 @@ static int dec_splits_for(int tiles, int nk) {
     return splits;
 }
 // decode-step weights are read once per step by one workgroup each: non-temporal LDS-DMA (aux = 2;
-// 3058-3070 vs 3053-3059 audio-s/s). WHISPER_MI355X_DEC_NT=0 restores the default policy (A/B).
+// 3058-3070 vs 3053-3059 audio-s/s). With the grid filled to <= 256 workgroups the default policy
+// measured 4-8 ms per step faster in one A/B (BENCH_KTIME=0) but the next bench on another box put
+// the cross-attention step at 90.9 instead of 86.1 us (profiles/r02_dec_nt_ab.txt); not adopted
+// without a same-box confirmation. WHISPER_MI355X_DEC_NT=0 selects the default policy (A/B).
 static bool dec_weight_nt() {
     static const bool on = [] {
         const char* e = getenv("WHISPER_MI355X_DEC_NT");
