@@ -66,9 +66,31 @@ def ensure_model(path: str, shape: str):
         log(f"[bench] wrote synthetic {shape} model to {path} in {time.time() - t:.1f}s")
 
 
+def cgroup_cpus():
+    """CPUs this job may use under its cgroup quota (cgroup v2 cpu.max "quota period", v1 cfs files),
+    or None when no quota caps it."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return dict(cpu_max=f"{q} {p}", cpus=int(q) / int(p))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        if q > 0:
+            return dict(cpu_max=f"{q} {p}", cpus=q / p)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_cpu() -> dict:
-    """The node's CPU as the driver box reports it (lscpu model name, logical CPUs) and the share
-    this job may use (OMP_NUM_THREADS on the box; the cgroup gives one GPU's job 16 CPUs)."""
+    """The node's CPU (lscpu model name, logical CPUs) and every CPU this job may use: the scheduler
+    affinity set, capped by the cgroup's CPU quota when one is set (cpu.max)."""
     model = None
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -77,8 +99,15 @@ def host_cpu() -> dict:
                 model = line.split(":", 1)[1].strip()
     except Exception:
         pass
-    share = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
-    return dict(model=model, logical_cpus=os.cpu_count(), affinity=len(os.sched_getaffinity(0)), share=share)
+    aff = len(os.sched_getaffinity(0))
+    cg = cgroup_cpus()
+    if cg is not None:
+        usable = max(1, min(aff, int(cg["cpus"])))
+    else:  # no quota visible: the box's declared share (it sets OMP_NUM_THREADS to the job's CPUs), else affinity
+        usable = min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff))
+    return dict(model=model, logical_cpus=os.cpu_count(), affinity=aff,
+                cgroup_cpu_max=cg["cpu_max"] if cg else None, usable=usable,
+                omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"))
 
 
 def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: int = 8) -> dict:
@@ -113,30 +142,32 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
                 sample=(f"1 x 30 s chunk: mel {t1 - t0:.2f}s + encoder/cross-KV {t2 - t1:.2f}s + prefill {t3 - t2:.2f}s "
                         f"+ {n_sample_tokens} decode steps ({per_step * 1e3:.0f} ms/step) measured, extrapolated to "
                         f"{n_tokens} steps/chunk; oracle/ = restated whisper.cpp CPU algorithm (not whisper.cpp), "
-                        f"{threads} OpenMP threads = this job's CPU share of a {cpu['logical_cpus']}-CPU "
-                        f"{cpu['model']} host"))
+                        f"{threads} OpenMP threads = every CPU this job may use (affinity {cpu['affinity']}, "
+                        f"cgroup cpu.max {cpu['cgroup_cpu_max']}) of a {cpu['logical_cpus']}-CPU {cpu['model']} host"))
 
 
-# kernel symbols of each class in the rocprofv3 PMC output (tools/pmc.sh -> tools/pmc_traffic.py)
-K_SYMBOL = {"gemm_encoder": r"gemm256_kernel", "attn_encoder": r"attn_enc2_kernel",
-            "attn_cross_decode": r"xattn_step_kernel"}
+# kernel symbol of each class in the rocprofv3 PMC output (tools/pmc.sh -> tools/pmc_traffic.py), per
+# cross-attention form for the decode-step class: straight from the encoder output, or the cached K/V
+K_SYMBOL = {("gemm_encoder", None): r"gemm8p_kernel", ("attn_encoder", None): r"attn_enc2_kernel",
+            ("attn_cross_decode", True): r"xattn_step_kernel", ("attn_cross_decode", False): r"attn_cross_step_kernel"}
 
 
-def pmc_traffic(kernel_class: str, grid_threads: int | None = None):
-    """Launch-weighted HBM bytes per launch of the class's kernel (restricted to launches of
-    `grid_threads` threads when given) from profiles/PMC_TRAFFIC_FILE (FETCH_SIZE doubled per the
-    gfx950 correction, + WRITE_SIZE), or None when that pass does not cover it."""
+def pmc_traffic(kernel_class: str, direct: bool | None, grid_threads: int | None):
+    """Launch-weighted HBM bytes per launch (FETCH_SIZE doubled per the gfx950 correction, +
+    WRITE_SIZE) of the kernel this class launched in the timed steps, from profiles/PMC_TRAFFIC_FILE:
+    matched by kernel symbol (and cross form) AND grid size, or None when that pass did not profile
+    this exact launch shape."""
     import re
-    pat = K_SYMBOL.get(kernel_class)
+    pat = K_SYMBOL.get((kernel_class, direct if kernel_class == "attn_cross_decode" else None))
     path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
-    if not pat or not os.path.exists(path):
+    if not pat or grid_threads is None or not os.path.exists(path):
         return None, None
     with open(path) as f:
         data = json.load(f)
     n = tb = 0.0
     for sym, v in data.items():
         name, _, grid = sym.partition("@grid=")
-        if re.search(pat, name) and (grid_threads is None or grid == str(grid_threads)):
+        if re.search(pat, name) and grid == str(grid_threads):
             n += v["launches"]
             tb += v["traffic_bytes"] * v["launches"]
     return (tb / n if n else None), PMC_TRAFFIC_FILE
@@ -270,6 +301,46 @@ def bench_frontend(wrs, ctx, buf, nb: int, n: int, reps: int = 5) -> dict:
     }
 
 
+def app_pattern(wrs, model_dir: str, shape: str, dtype: str, calls: int) -> dict:
+    """The reference app's own call pattern, per call (src-tauri/src/state.rs:147 streaming worker ->
+    whisper.rs:66-148 through the C++ mirror of WhisperEngine, host/whisper_engine.cpp): a fresh
+    whisper_state per call (whisper.rs:83-85), one <= 25.2 s chunk (audio.rs:11,15: forced cut at 25 s +
+    200 ms overlap), language "auto" (config.rs:49), initial prompt = the default vocabulary + the
+    previous chunk's text (config.rs:40-42, whisper.rs:98-105, state.rs:144-151), segments joined and
+    filtered. Latency per call = host wall clock around transcribe (PCM on the host, results on the
+    host). Measured with the context's state pool (default: a released state keeps its workspace and
+    decode graphs for the next call) and without it (WHISPER_MI355X_STATE_POOL=0: every call allocates
+    its workspace and captures its decode graphs, as a plain whisper.cpp state would)."""
+    import numpy as np
+    from make_model import synthetic_pcm
+    path = os.path.join(model_dir, f"{shape}_s0.bin")
+    ensure_model(path, shape)
+    os.environ["WHISPER_MI355X_DTYPE"] = dtype
+    chunks = [synthetic_pcm(100 + k, seconds=25.2) for k in range(calls)]
+    out = {"model": shape, "dtype": dtype, "chunk_s": 25.2, "calls": calls}
+    for label, pool in (("state_pool", "2"), ("no_pool", "0")):
+        os.environ["WHISPER_MI355X_STATE_POOL"] = pool
+        eng = wrs.WhisperEngine()
+        assert eng.load_model(path) == 0
+        last, lat, chars = None, [], 0
+        for x in chunks:
+            t = time.perf_counter()
+            rc, text = eng.transcribe(x, None, wrs.DEFAULT_VOCABULARY, last)
+            lat.append(time.perf_counter() - t)
+            assert rc == 0, rc
+            last = text or None
+            chars += len(text or "")
+        del eng
+        steady = sorted(lat[1:]) or lat
+        out[label] = dict(first_call_ms=round(lat[0] * 1e3, 1), median_ms=round(1e3 * steady[len(steady) // 2], 1),
+                          min_ms=round(1e3 * min(steady), 1),
+                          rtf_inverse_median=round(25.2 / steady[len(steady) // 2], 1))
+    out["text_chars_total"] = chars
+    os.environ.pop("WHISPER_MI355X_STATE_POOL", None)
+    os.environ.pop("WHISPER_MI355X_DTYPE", None)
+    return out
+
+
 def _wall(fn) -> float:
     t = time.perf_counter()
     fn()
@@ -292,8 +363,16 @@ def main():
     ap.add_argument("--variant-steps", type=int, default=3)
     ap.add_argument("--frontend", type=int, default=1,
                     help="also time the GPU audio front-end (audio.rs VAD chunking + 48 kHz -> 16 kHz resampler)")
+    ap.add_argument("--app-pattern", type=int, default=1,
+                    help="also time the app's per-call pattern (fresh state per 25 s chunk, whisper.rs:66-148) "
+                         "on base f16 and this model in its dtype (rank 0)")
+    ap.add_argument("--app-calls", type=int, default=6)
+    ap.add_argument("--weights", default="conf", choices=["conf", "plain"],
+                    help="synthetic weight init: conf = a decoder as peaked as a trained one (tools/make_model.py "
+                         "+conf), so real greedy termination happens; plain = i.i.d. random")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this job's CPU share (OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this job may use (affinity, capped by the cgroup cpu.max quota)")
     ap.add_argument("--model-dir", default=os.environ.get("NW_MODEL_DIR", "/tmp/nw_models"))
     ap.add_argument("--plan", action="store_true",
                     help="CPU dry run of the rank layout: gloo group, shard map and max-over-ranks, no GPU")
@@ -321,9 +400,10 @@ def main():
 
     wrs = load_wrs()
     os.makedirs(args.model_dir, exist_ok=True)
-    model_path = os.path.join(args.model_dir, f"{args.model}_s0.bin")
+    shape = args.model + ("+conf" if args.weights == "conf" else "")
+    model_path = os.path.join(args.model_dir, f"{shape}_s0.bin")
     if local_rank == 0:
-        ensure_model(model_path, args.model)
+        ensure_model(model_path, shape)
     barrier()
 
     # ---- context: rank 0 loads, the others receive the weight arena over RCCL (xGMI) -------------
@@ -364,17 +444,17 @@ def main():
         L.whisper_mi355x_memcpy(ctx.ptr, C.c_void_p(buf + i * n * 4), host.ctypes.data, n * 4, 1)
     jobs = [(buf + i * n * 4, n) for i in range(nb)]
 
-    def step(params):
+    def step(params, fixed=None):
         if nb:
-            rc = st.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
+            rc = st.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens if fixed is None else fixed)
             assert rc == 0, rc
 
-    def timed(params, steps):
+    def timed(params, steps, fixed=None):
         barrier()
         torch.cuda.synchronize()
         t0 = time.time()
         for _ in range(steps):
-            step(params)
+            step(params, fixed)
         torch.cuda.synchronize()
         barrier()
         return max_over_ranks(time.time() - t0, dist, "cuda")
@@ -427,10 +507,25 @@ def main():
                                  ms_per_step=round(1e3 * el / args.variant_steps, 2),
                                  prompt_tokens=len(ctx.tokenize(wrs.DEFAULT_VOCABULARY)) if "vocabulary" in name else 0,
                                  phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
+        # SURVEY.md §8d's second mode: real greedy termination (EOT and timestamps end each window, the
+        # reference's temperature fallback on: whisper.rs:88-124 verbatim), same chunks, same weights
+        p = wrs.reference_full_params("en")
+        step(p, 0)
+        el = timed(p, args.variant_steps, 0)
+        dec_tok = L.whisper_mi355x_batch_decoded_tokens(st.ptr)
+        fell_back = sum(1 for j in range(nb) for d in st.decisions(j) if d["temp_idx"] > 0)
+        variants.append(dict(workload="real greedy termination (EOT / timestamps end each window; fallback on; "
+                                      "language en, no prompt)",
+                             value=round(30.0 * global_batch * args.variant_steps / el, 2),
+                             ms_per_step=round(1e3 * el / args.variant_steps, 2),
+                             decoded_tokens_per_chunk=round(dec_tok / max(1, nb), 1),
+                             windows_fallen_back=fell_back,
+                             phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
 
     frontend = None
     if args.frontend and rank == 0 and nb:
         frontend = bench_frontend(wrs, ctx, buf, nb, n)
+    form = st.info()  # the cross-attention form of the timed steps' last call (PMC lookup below)
 
     if rank == 0:
         audio_s = 30.0 * global_batch * args.steps
@@ -446,9 +541,10 @@ def main():
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
         grid = None
-        if K_NAMES[dom] == "attn_cross_decode":  # decode-step launches: splits x clips workgroups of 512
+        if K_NAMES[dom] == "attn_cross_decode" and form["direct"]:
+            # decode-step launches of xattn_step_kernel: splits x clips workgroups of 512 threads
             grid = max(1, min(16, -(-256 // nb))) * nb * 512
-        traffic, src = pmc_traffic(K_NAMES[dom], grid)
+        traffic, src = pmc_traffic(K_NAMES[dom], form["direct"], grid)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                         traffic_source=f"profiles/{src}")
@@ -456,7 +552,7 @@ def main():
                     work_per_launch=k_work / max(1, k_cnt), time_share_warmup=share)
         # per-phase, time-weighted rooflines of rank 0's last step (phase clocks are host wall time
         # around stream-synchronised phases)
-        pw = phase_work(args.model, nb, args.tokens, 3, True)
+        pw = phase_work(args.model, nb, args.tokens, 3, form["direct"])
         enc_s = phases["encode"] * 1e-3
         dec_s = phases["decode"] * 1e-3
         mfma_peak = FP8_PEAK_TFS if args.dtype == "fp8" else MFMA_PEAK_TFS
@@ -473,9 +569,18 @@ def main():
                            frac=round(pw["dec_bytes_per_step"] * (args.tokens - 1) / max(1e-9, dec_s) / 1e9 / HBM_PEAK_GBS, 4),
                            bytes_split_gb={k: round(pw[k] / 1e9, 3) for k in ("dec_weight_bytes", "dec_cross_bytes", "dec_self_bytes")}),
         }
+        app = None
+        if args.app_pattern:
+            app = []
+            try:
+                app.append(app_pattern(wrs, args.model_dir, "base+conf", "f16", args.app_calls))
+                app.append(app_pattern(wrs, args.model_dir, shape, "bf16" if args.dtype != "f16" else "f16",
+                                       args.app_calls))
+            except Exception as e:  # reported, never fatal to the GPU number
+                app.append(dict(error=str(e)))
         cpu = None
-        if args.cpu_baseline and world == 1:
-            threads = args.cpu_threads or host_cpu()["share"]
+        if args.cpu_baseline:
+            threads = args.cpu_threads or host_cpu()["usable"]
             try:
                 cpu = cpu_baseline(model_path, threads, args.tokens)
             except Exception as e:  # reported, never fatal to the GPU number
@@ -485,7 +590,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "audio-sec/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 2), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic (seeded AM-harmonic 30 s PCM; seeded random weights of the named architecture)",
+            "data": ("synthetic (seeded AM-harmonic 30 s PCM; seeded random weights of the named architecture"
+                     + (", decoder init as peaked as a trained model's: tools/make_model.py +conf)" if args.weights == "conf"
+                        else ")")),
             "config": {"workload": f"{args.model} {args.dtype} greedy, {global_batch} x 30 s chunks per step over "
                                    f"{world} GPU(s) ({nb} on rank 0), fixed {args.tokens}-token decode per chunk, "
                                    f"language en, no prompt",
@@ -495,7 +602,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "variants": variants,
+            "app_pattern": app,
             "extra": {"rtf_inverse_per_gpu": round(value / world, 2), "decoded_tokens_per_step": decoded,
+                      "cross_form": "direct" if form["direct"] else "cache",
                       "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
                       "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),
                       "weight_broadcast_s": round(bcast_s, 3), "frontend": frontend},

@@ -15,6 +15,12 @@
 extern "C" {
 #endif
 
+/* Return code of every entry point below (and of whisper_full_with_state / whisper_pcm_to_mel /
+ * whisper_encode / whisper_decode) when the engine hit a device error (a HIP error such as out of
+ * memory) or an unsupported shape: the call is abandoned, nothing is aborted, and the context and
+ * the state stay usable (whisper.rs:127-129 maps any non-zero return to TranscriptionError). */
+#define WHISPER_MI355X_ERR_RUNTIME (-10)
+
 /* compute type of weights and GEMM activations. FP8_ENC: bf16, with the encoder's QKV, FC1 and FC2
  * GEMMs on OCP e4m3 weights and activations (per-row f32 scales; the large-v3-turbo fp8 config).
  * FP8_ENC is a throughput mode, not a whisper.cpp-parity mode. */
@@ -167,6 +173,13 @@ WHISPER_API int whisper_mi355x_resample_operator(int rate_in, int * fsi, int * f
  * sizeof(whisper_token_data), offsetof(full_params, initial_prompt / language / greedy /
  * new_segment_callback / vad_params). Lets a binding (bindgen, ctypes) be checked field-by-field. */
 WHISPER_API int whisper_mi355x_abi_layout(size_t out[8]);
+
+/* State introspection (tests): out[0] = cross-attention form of the last call (1 = straight from the
+ * encoder output, 0 = cached cross K/V), out[1] = clip slots of the workspace, out[2] = slots of the
+ * cross K/V cache, out[3] = decode-step graphs kept, out[4] = 1 if the state was recycled from the
+ * context's state pool (whisper_init_state after a whisper_free_state keeps the workspace and the
+ * captured decode graphs; WHISPER_MI355X_STATE_POOL=0 disables the pool). Returns 5. */
+WHISPER_API int whisper_mi355x_state_info(struct whisper_state * state, int out[5]);
 
 /* HIP stream of a state (hipStream_t), for callers that enqueue their own work around it. */
 WHISPER_API void * whisper_mi355x_state_stream(struct whisper_state * state);

@@ -168,50 +168,62 @@ const float* const* stage_inputs(DeviceScratch* S, char* base, size_t* off, cons
 
 using namespace wm;
 
+// engine errors (a HIP error, a rate whose 20 ms window does not fit the kernel's LDS) -> -1
+template <typename F> static int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const wm::Error&) {
+    } catch (const std::bad_alloc&) {
+    }
+    return -1;
+}
+
 extern "C" {
 
 int whisper_mi355x_find_silence_boundaries(int device, const float* const* pcm, const int* n_samples, int n_clips,
                                            int sample_rate, bool pcm_on_device, int* counts, int* boundaries, int cap,
                                            float* noise_floor, float* rms_out, int rms_stride) {
-    if (n_clips <= 0) return 0;
-    if (!pcm || !n_samples || !counts || cap < 0 || sample_rate < 50) return -1;
-    const int ws = sample_rate / 50;
-    int max_n = 0;
-    size_t in_bytes = 0;
-    for (int c = 0; c < n_clips; c++) {
-        if (n_samples[c] < 0) return -1;
-        max_n = std::max(max_n, n_samples[c]);
-        in_bytes += align256((size_t)std::max(n_samples[c], 1) * 4);
-    }
-    const int max_win = std::max(1, max_n / ws);
-    if (rms_out && rms_stride < max_n / ws) return -1;
-    DeviceGuard g(device);
-    DeviceScratch* S = scratch(device);
-    std::lock_guard<std::mutex> lk(S->mu);
-    const size_t bytes = (pcm_on_device ? 0 : in_bytes) + align256(sizeof(float*) * n_clips) +
-                         align256((size_t)n_clips * max_win * 4) + 2 * align256((size_t)n_clips * 4) +
-                         align256((size_t)n_clips * std::max(cap, 1) * 4);
-    char* base = S->get(bytes);
-    size_t off = 0;
-    std::vector<const float*> ptrs;
-    const float* const* d_pcm = stage_inputs(S, base, &off, pcm, n_samples, n_clips, pcm_on_device, ptrs);
-    int* d_n = (int*)(base + off); off += align256((size_t)n_clips * 4);
-    float* d_rms = (float*)(base + off); off += align256((size_t)n_clips * max_win * 4);
-    int* d_counts = (int*)(base + off); off += align256((size_t)n_clips * 4);
-    float* d_floor = (float*)(base + off); off += align256((size_t)n_clips * 4);
-    int* d_b = (int*)(base + off);
-    WM_CHECK(hipMemcpyAsync(d_n, n_samples, (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
-    launch_silence_boundaries(d_pcm, d_n, n_clips, max_n, sample_rate, d_rms, max_win, d_counts, d_b, std::max(cap, 1),
-                              d_floor, S->st);
-    WM_CHECK(hipMemcpyAsync(counts, d_counts, (size_t)n_clips * 4, hipMemcpyDeviceToHost, S->st));
-    if (cap > 0 && boundaries)
-        WM_CHECK(hipMemcpyAsync(boundaries, d_b, (size_t)n_clips * cap * 4, hipMemcpyDeviceToHost, S->st));
-    if (noise_floor) WM_CHECK(hipMemcpyAsync(noise_floor, d_floor, (size_t)n_clips * 4, hipMemcpyDeviceToHost, S->st));
-    if (rms_out)
-        WM_CHECK(hipMemcpy2DAsync(rms_out, (size_t)rms_stride * 4, d_rms, (size_t)max_win * 4, (size_t)(max_n / ws) * 4,
-                                  n_clips, hipMemcpyDeviceToHost, S->st));
-    WM_CHECK(hipStreamSynchronize(S->st));
-    return 0;
+    return guarded([&]() -> int {
+        if (n_clips <= 0) return 0;
+        if (!pcm || !n_samples || !counts || cap < 0 || sample_rate < 50) return -1;
+        const int ws = sample_rate / 50;
+        int max_n = 0;
+        size_t in_bytes = 0;
+        for (int c = 0; c < n_clips; c++) {
+            if (n_samples[c] < 0) return -1;
+            max_n = std::max(max_n, n_samples[c]);
+            in_bytes += align256((size_t)std::max(n_samples[c], 1) * 4);
+        }
+        const int max_win = std::max(1, max_n / ws);
+        if (rms_out && rms_stride < max_n / ws) return -1;
+        DeviceGuard g(device);
+        DeviceScratch* S = scratch(device);
+        std::lock_guard<std::mutex> lk(S->mu);
+        const size_t bytes = (pcm_on_device ? 0 : in_bytes) + align256(sizeof(float*) * n_clips) +
+                             align256((size_t)n_clips * max_win * 4) + 2 * align256((size_t)n_clips * 4) +
+                             align256((size_t)n_clips * std::max(cap, 1) * 4);
+        char* base = S->get(bytes);
+        size_t off = 0;
+        std::vector<const float*> ptrs;
+        const float* const* d_pcm = stage_inputs(S, base, &off, pcm, n_samples, n_clips, pcm_on_device, ptrs);
+        int* d_n = (int*)(base + off); off += align256((size_t)n_clips * 4);
+        float* d_rms = (float*)(base + off); off += align256((size_t)n_clips * max_win * 4);
+        int* d_counts = (int*)(base + off); off += align256((size_t)n_clips * 4);
+        float* d_floor = (float*)(base + off); off += align256((size_t)n_clips * 4);
+        int* d_b = (int*)(base + off);
+        WM_CHECK(hipMemcpyAsync(d_n, n_samples, (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
+        launch_silence_boundaries(d_pcm, d_n, n_clips, max_n, sample_rate, d_rms, max_win, d_counts, d_b, std::max(cap, 1),
+                                  d_floor, S->st);
+        WM_CHECK(hipMemcpyAsync(counts, d_counts, (size_t)n_clips * 4, hipMemcpyDeviceToHost, S->st));
+        if (cap > 0 && boundaries)
+            WM_CHECK(hipMemcpyAsync(boundaries, d_b, (size_t)n_clips * cap * 4, hipMemcpyDeviceToHost, S->st));
+        if (noise_floor) WM_CHECK(hipMemcpyAsync(noise_floor, d_floor, (size_t)n_clips * 4, hipMemcpyDeviceToHost, S->st));
+        if (rms_out)
+            WM_CHECK(hipMemcpy2DAsync(rms_out, (size_t)rms_stride * 4, d_rms, (size_t)max_win * 4, (size_t)(max_n / ws) * 4,
+                                      n_clips, hipMemcpyDeviceToHost, S->st));
+        WM_CHECK(hipStreamSynchronize(S->st));
+        return 0;
+    });
 }
 
 int whisper_mi355x_resample_len(int n_in, int rate_in) {
@@ -226,62 +238,64 @@ int whisper_mi355x_resample_len(int n_in, int rate_in) {
 
 int whisper_mi355x_resample_chunk(int device, const float* const* audio, const int* n_in, int n_clips, int rate_in,
                                   bool on_device, float* const* out) {
-    if (n_clips <= 0) return 0;
-    if (!audio || !n_in || !out || rate_in <= 0) return -1;
-    DeviceGuard g(device);
-    DeviceScratch* S = scratch(device);
-    std::lock_guard<std::mutex> lk(S->mu);
-    std::vector<int> n_out(n_clips);
-    int max_out = 0;
-    size_t in_bytes = 0, out_bytes = 0;
-    for (int c = 0; c < n_clips; c++) {
-        if (n_in[c] < 0) return -1;
-        n_out[c] = whisper_mi355x_resample_len(n_in[c], rate_in);
-        max_out = std::max(max_out, n_out[c]);
-        in_bytes += align256((size_t)std::max(n_in[c], 1) * 4);
-        out_bytes += align256((size_t)std::max(n_out[c], 1) * 4);
-    }
-    if (rate_in == kRate) {  // resample_chunk returns the audio unchanged (audio.rs:332-334)
+    return guarded([&]() -> int {
+        if (n_clips <= 0) return 0;
+        if (!audio || !n_in || !out || rate_in <= 0) return -1;
+        DeviceGuard g(device);
+        DeviceScratch* S = scratch(device);
+        std::lock_guard<std::mutex> lk(S->mu);
+        std::vector<int> n_out(n_clips);
+        int max_out = 0;
+        size_t in_bytes = 0, out_bytes = 0;
         for (int c = 0; c < n_clips; c++) {
-            if (n_in[c] <= 0) continue;
-            if (on_device) WM_CHECK(hipMemcpyAsync(out[c], audio[c], (size_t)n_in[c] * 4, hipMemcpyDeviceToDevice, S->st));
-            else std::memcpy(out[c], audio[c], (size_t)n_in[c] * 4);
+            if (n_in[c] < 0) return -1;
+            n_out[c] = whisper_mi355x_resample_len(n_in[c], rate_in);
+            max_out = std::max(max_out, n_out[c]);
+            in_bytes += align256((size_t)std::max(n_in[c], 1) * 4);
+            out_bytes += align256((size_t)std::max(n_out[c], 1) * 4);
         }
+        if (rate_in == kRate) {  // resample_chunk returns the audio unchanged (audio.rs:332-334)
+            for (int c = 0; c < n_clips; c++) {
+                if (n_in[c] <= 0) continue;
+                if (on_device) WM_CHECK(hipMemcpyAsync(out[c], audio[c], (size_t)n_in[c] * 4, hipMemcpyDeviceToDevice, S->st));
+                else std::memcpy(out[c], audio[c], (size_t)n_in[c] * 4);
+            }
+            WM_CHECK(hipStreamSynchronize(S->st));
+            return 0;
+        }
+        ResampleOp& op = S->ops[rate_in];
+        if (!op.dW) {
+            const FftSizes z = fft_sizes(rate_in);
+            op.fsi = z.fsi; op.fso = z.fso; op.ldw = (z.fso + 63) / 64 * 64;
+            const std::vector<float> W = fft_fixed_in_operator(op.fsi, op.fso, op.ldw);
+            WM_CHECK(hipMalloc((void**)&op.dW, W.size() * 4));
+            WM_CHECK(hipMemcpy(op.dW, W.data(), W.size() * 4, hipMemcpyHostToDevice));
+        }
+        const size_t bytes = (on_device ? 0 : in_bytes + out_bytes) + 2 * align256(sizeof(float*) * n_clips) +
+                             2 * align256((size_t)n_clips * 4);
+        char* base = S->get(bytes);
+        size_t off = 0;
+        std::vector<const float*> ptrs;
+        const float* const* d_in = stage_inputs(S, base, &off, audio, n_in, n_clips, on_device, ptrs);
+        std::vector<float*> optr(n_clips);
+        for (int c = 0; c < n_clips; c++) {
+            if (on_device) optr[c] = out[c];
+            else { optr[c] = (float*)(base + off); off += align256((size_t)std::max(n_out[c], 1) * 4); }
+        }
+        float** d_out = (float**)(base + off); off += align256(sizeof(float*) * n_clips);
+        int* d_nin = (int*)(base + off); off += align256((size_t)n_clips * 4);
+        int* d_nout = (int*)(base + off);
+        WM_CHECK(hipMemcpyAsync(d_out, optr.data(), sizeof(float*) * n_clips, hipMemcpyHostToDevice, S->st));
+        WM_CHECK(hipMemcpyAsync(d_nin, n_in, (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
+        WM_CHECK(hipMemcpyAsync(d_nout, n_out.data(), (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
+        launch_resample(d_in, d_nin, n_clips, max_out, op.dW, op.ldw, op.fsi, op.fso, d_out, d_nout, S->st);
+        if (!on_device)
+            for (int c = 0; c < n_clips; c++)
+                if (n_out[c] > 0)
+                    WM_CHECK(hipMemcpyAsync(out[c], optr[c], (size_t)n_out[c] * 4, hipMemcpyDeviceToHost, S->st));
         WM_CHECK(hipStreamSynchronize(S->st));
         return 0;
-    }
-    ResampleOp& op = S->ops[rate_in];
-    if (!op.dW) {
-        const FftSizes z = fft_sizes(rate_in);
-        op.fsi = z.fsi; op.fso = z.fso; op.ldw = (z.fso + 63) / 64 * 64;
-        const std::vector<float> W = fft_fixed_in_operator(op.fsi, op.fso, op.ldw);
-        WM_CHECK(hipMalloc((void**)&op.dW, W.size() * 4));
-        WM_CHECK(hipMemcpy(op.dW, W.data(), W.size() * 4, hipMemcpyHostToDevice));
-    }
-    const size_t bytes = (on_device ? 0 : in_bytes + out_bytes) + 2 * align256(sizeof(float*) * n_clips) +
-                         2 * align256((size_t)n_clips * 4);
-    char* base = S->get(bytes);
-    size_t off = 0;
-    std::vector<const float*> ptrs;
-    const float* const* d_in = stage_inputs(S, base, &off, audio, n_in, n_clips, on_device, ptrs);
-    std::vector<float*> optr(n_clips);
-    for (int c = 0; c < n_clips; c++) {
-        if (on_device) optr[c] = out[c];
-        else { optr[c] = (float*)(base + off); off += align256((size_t)std::max(n_out[c], 1) * 4); }
-    }
-    float** d_out = (float**)(base + off); off += align256(sizeof(float*) * n_clips);
-    int* d_nin = (int*)(base + off); off += align256((size_t)n_clips * 4);
-    int* d_nout = (int*)(base + off);
-    WM_CHECK(hipMemcpyAsync(d_out, optr.data(), sizeof(float*) * n_clips, hipMemcpyHostToDevice, S->st));
-    WM_CHECK(hipMemcpyAsync(d_nin, n_in, (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
-    WM_CHECK(hipMemcpyAsync(d_nout, n_out.data(), (size_t)n_clips * 4, hipMemcpyHostToDevice, S->st));
-    launch_resample(d_in, d_nin, n_clips, max_out, op.dW, op.ldw, op.fsi, op.fso, d_out, d_nout, S->st);
-    if (!on_device)
-        for (int c = 0; c < n_clips; c++)
-            if (n_out[c] > 0)
-                WM_CHECK(hipMemcpyAsync(out[c], optr[c], (size_t)n_out[c] * 4, hipMemcpyDeviceToHost, S->st));
-    WM_CHECK(hipStreamSynchronize(S->st));
-    return 0;
+    });
 }
 
 int whisper_mi355x_resample_operator(int rate_in, int* fsi, int* fso, float* W, long cap) {

@@ -15,6 +15,21 @@ using namespace wm;
 
 static Context* C(whisper_context* ctx) { return ctx ? &ctx->c : nullptr; }
 
+// Engine errors (wm::Error: a HIP error such as out of memory, an unsupported shape) end the call
+// with WHISPER_MI355X_ERR_RUNTIME and leave the context and the state usable; whisper-rs turns the
+// non-zero return into WhisperError (whisper.rs:127-129) and the app logs and skips the chunk
+// (state.rs:157-159).
+template <typename F> static int guarded(whisper_state* s, F&& f) {
+    try {
+        return f();
+    } catch (const wm::Error&) {
+    } catch (const std::bad_alloc&) {
+        fprintf(stderr, "whisper_mi355x: host out of memory\n");
+    }
+    if (s) recover_state(s);
+    return WHISPER_MI355X_ERR_RUNTIME;
+}
+
 static DType env_dtype(DType def) {
     const char* e = getenv("WHISPER_MI355X_DTYPE");
     if (!e) return def;
@@ -32,7 +47,13 @@ static whisper_context* make_ctx(const char* path, whisper_context_params cp, in
     // dtype 2 = bf16 with the fp8 encoder GEMMs (large-v3-turbo fp8 config)
     w->c.fp8_enc = dtype == 2;
     if (dtype == 2) dtype = (int)DType::BF16;
-    if (!load_context(&w->c, path, dev, (DType)dtype, load)) {
+    bool ok = false;
+    try {
+        ok = load_context(&w->c, path, dev, (DType)dtype, load);
+    } catch (const wm::Error&) {
+    } catch (const std::bad_alloc&) {
+    }
+    if (!ok) {
         free_context(&w->c);
         delete w;
         return nullptr;
@@ -131,7 +152,8 @@ struct whisper_context* whisper_init_from_file_with_params_no_state(const char* 
 }
 struct whisper_context* whisper_init_from_file_with_params(const char* path, struct whisper_context_params p) {
     whisper_context* w = whisper_init_from_file_with_params_no_state(path, p);
-    if (w) w->c.default_state = new_state(&w->c);
+    if (w) w->c.default_state = whisper_init_state(w);
+    if (w && !w->c.default_state) { whisper_free(w); return nullptr; }
     return w;
 }
 struct whisper_context* whisper_init_from_buffer_with_params_no_state(void*, size_t, struct whisper_context_params) {
@@ -150,7 +172,9 @@ struct whisper_context* whisper_init_with_params(struct whisper_model_loader* l,
 }
 struct whisper_state* whisper_init_state(struct whisper_context* ctx) {
     if (!ctx) return nullptr;
-    return new_state(&ctx->c);
+    whisper_state* s = nullptr;
+    guarded(nullptr, [&] { s = new_state(&ctx->c); return 0; });
+    return s;
 }
 int whisper_ctx_init_openvino_encoder_with_state(struct whisper_context*, struct whisper_state*, const char*, const char*, const char*) { return 1; }
 int whisper_ctx_init_openvino_encoder(struct whisper_context*, const char*, const char*, const char*) { return 1; }
@@ -159,6 +183,7 @@ void whisper_free(struct whisper_context* ctx) {
     if (!ctx) return;
     if (ctx->c.default_state) free_state(ctx->c.default_state);
     ctx->c.default_state = nullptr;
+    drain_state_pool(&ctx->c);
     free_context(&ctx->c);  // weight arena + the fp8 arena
     delete ctx;
 }
@@ -169,7 +194,7 @@ int whisper_pcm_to_mel_with_state(struct whisper_context* ctx, struct whisper_st
     hipSetDevice(ctx->c.device);
     const float* pp[1] = {samples};
     int nn[1] = {n};
-    return compute_mel(&ctx->c, s, pp, nn, 1, false);
+    return guarded(s, [&] { return compute_mel(&ctx->c, s, pp, nn, 1, false); });
 }
 int whisper_pcm_to_mel(struct whisper_context* ctx, const float* samples, int n, int t) {
     return whisper_pcm_to_mel_with_state(ctx, ctx ? ctx->c.default_state : nullptr, samples, n, t);
@@ -180,29 +205,31 @@ int whisper_set_mel_with_state(struct whisper_context*, struct whisper_state*, c
 }
 int whisper_set_mel(struct whisper_context* ctx, const float* d, int n, int m) { return whisper_set_mel_with_state(ctx, nullptr, d, n, m); }
 int whisper_encode_with_state(struct whisper_context* ctx, struct whisper_state* s, int offset, int) {
-    if (!ctx || !s || s->ws.cap_jobs < 1) return -1;
+    if (!ctx || !s || !s->mel_ready) return -1;
     hipSetDevice(ctx->c.device);
     int job = 0, slot = 0;
-    return encode_windows(&ctx->c, s, &job, &offset, &slot, 1);
+    return guarded(s, [&] { return encode_windows(&ctx->c, s, &job, &offset, &slot, 1); });
 }
 int whisper_encode(struct whisper_context* ctx, int offset, int t) {
     return whisper_encode_with_state(ctx, ctx ? ctx->c.default_state : nullptr, offset, t);
 }
 int whisper_decode_with_state(struct whisper_context* ctx, struct whisper_state* s, const whisper_token* tokens, int n_tokens,
                               int n_past, int) {
-    if (!ctx || !s || s->ws.cap_jobs < 1 || n_tokens <= 0) return -1;
+    if (!ctx || !s || !s->mel_ready || n_tokens <= 0) return -1;
     if (n_past + n_tokens > ctx->c.hp.n_text_ctx) return -1;
     hipSetDevice(ctx->c.device);
     std::vector<int> pos(n_tokens), slot(n_tokens, 0);
     for (int i = 0; i < n_tokens; i++) pos[i] = n_past + i;
     int row = n_tokens - 1;
-    if (decode_tokens(&ctx->c, s, tokens, pos.data(), slot.data(), n_tokens, &row, 1) != 0) return -1;
-    const int V = ctx->c.hp.n_vocab;
-    s->logits_host.assign((size_t)n_tokens * V, 0.0f);
-    WM_CHECK(hipMemcpyAsync(s->logits_host.data() + (size_t)(n_tokens - 1) * V, s->ws.logits, (size_t)V * 4,
-                            hipMemcpyDeviceToHost, s->stream));
-    WM_CHECK(hipStreamSynchronize(s->stream));
-    return 0;
+    return guarded(s, [&] {
+        if (decode_tokens(&ctx->c, s, tokens, pos.data(), slot.data(), n_tokens, &row, 1) != 0) return -1;
+        const int V = ctx->c.hp.n_vocab;
+        s->logits_host.assign((size_t)n_tokens * V, 0.0f);
+        WM_CHECK(hipMemcpyAsync(s->logits_host.data() + (size_t)(n_tokens - 1) * V, s->ws.logits, (size_t)V * 4,
+                                hipMemcpyDeviceToHost, s->stream));
+        WM_CHECK(hipStreamSynchronize(s->stream));
+        return 0;
+    });
 }
 int whisper_decode(struct whisper_context* ctx, const whisper_token* t, int n, int n_past, int th) {
     return whisper_decode_with_state(ctx, ctx ? ctx->c.default_state : nullptr, t, n, n_past, th);
@@ -226,17 +253,21 @@ int whisper_lang_id(const char* lang) { return lang_index(lang); }
 const char* whisper_lang_str(int id) { return id >= 0 && id < 100 ? k_lang_codes[id] : nullptr; }
 const char* whisper_lang_str_full(int id) { return id >= 0 && id < 100 ? k_lang_names[id] : nullptr; }
 int whisper_lang_auto_detect_with_state(struct whisper_context* ctx, struct whisper_state* s, int offset_ms, int, float* probs) {
-    if (!ctx || !s) return -1;
+    if (!ctx || !s || !s->mel_ready) return -1;
     const int seek = offset_ms / 10;
     if (seek < 0 || seek >= s->n_len_org) return -2;
     hipSetDevice(ctx->c.device);
     int job = 0, slot = 0;
-    if (encode_windows(&ctx->c, s, &job, &seek, &slot, 1) != 0) return -6;
     const Vocab& v = ctx->c.vocab;
-    int tok = v.token_sot, pos = 0, row = 0;
-    if (decode_tokens(&ctx->c, s, &tok, &pos, &slot, 1, &row, 1) != 0) return -7;
     std::vector<float> lg(100);
-    WM_CHECK(hipMemcpy(lg.data(), s->ws.logits + v.token_sot + 1, 100 * 4, hipMemcpyDeviceToHost));
+    const int rc = guarded(s, [&] {
+        if (encode_windows(&ctx->c, s, &job, &seek, &slot, 1) != 0) return -6;
+        int tok = v.token_sot, pos = 0, row = 0;
+        if (decode_tokens(&ctx->c, s, &tok, &pos, &slot, 1, &row, 1) != 0) return -7;
+        WM_CHECK(hipMemcpy(lg.data(), s->ws.logits + v.token_sot + 1, 100 * 4, hipMemcpyDeviceToHost));
+        return 0;
+    });
+    if (rc != 0) return rc;
     std::map<std::string, int> g_lang;
     for (int i = 0; i < 100; i++) g_lang[k_lang_codes[i]] = i;
     std::vector<std::pair<float, int>> ids;
@@ -307,7 +338,7 @@ int whisper_full_with_state(struct whisper_context* ctx, struct whisper_state* s
     const float* pp[1] = {samples};
     int nn[1] = {n_samples};
     FullOpts o;
-    return full_batch(&ctx->c, s, p, pp, nn, 1, false, o, true);
+    return guarded(s, [&] { return full_batch(&ctx->c, s, p, pp, nn, 1, false, o, true); });
 }
 int whisper_full(struct whisper_context* ctx, struct whisper_full_params p, const float* samples, int n) {
     return whisper_full_with_state(ctx, ctx ? ctx->c.default_state : nullptr, p, samples, n);
@@ -395,12 +426,17 @@ int whisper_mi355x_broadcast_weights(struct whisper_context* ctx, const char uid
     memcpy(&id, uid, 128);
     ncclComm_t comm;
     if (ncclCommInitRank(&comm, world, id, rank) != ncclSuccess) return -2;
-    hipStream_t st;
-    WM_CHECK(hipStreamCreate(&st));
-    ncclResult_t r = ncclBroadcast(ctx->c.arena, ctx->c.arena, ctx->c.arena_bytes, ncclChar, 0, comm, st);
-    WM_CHECK(hipStreamSynchronize(st));
-    WM_CHECK(hipStreamDestroy(st));
+    hipStream_t st = nullptr;
+    ncclResult_t r = ncclInternalError;
+    const int rc = guarded(nullptr, [&] {
+        WM_CHECK(hipStreamCreate(&st));
+        r = ncclBroadcast(ctx->c.arena, ctx->c.arena, ctx->c.arena_bytes, ncclChar, 0, comm, st);
+        WM_CHECK(hipStreamSynchronize(st));
+        return 0;
+    });
+    if (st) hipStreamDestroy(st);
     ncclCommDestroy(comm);
+    if (rc != 0) return rc;
     return r == ncclSuccess ? 0 : -3;
 }
 
@@ -409,7 +445,7 @@ int whisper_mi355x_full_batch(struct whisper_context* ctx, struct whisper_state*
     if (!ctx || !s || n_jobs <= 0) return -1;
     FullOpts o;
     o.fixed_tokens = fixed_tokens;
-    return full_batch(&ctx->c, s, p, pcm, n, n_jobs, on_device, o, false);
+    return guarded(s, [&] { return full_batch(&ctx->c, s, p, pcm, n, n_jobs, on_device, o, false); });
 }
 int whisper_mi355x_batch_n_segments(struct whisper_state* s, int job) {
     return s && job >= 0 && job < (int)s->results.size() ? (int)s->results[job].size() : 0;
@@ -436,35 +472,48 @@ int whisper_mi355x_phase_ms(struct whisper_state* s, double out[5]) {
     return 0;
 }
 int whisper_mi355x_get_mel(struct whisper_state* s, float* out, int cap) {
-    if (!s || !s->ws.mel) return -1;
-    Context* c = s->ctx;
-    const int nm = c->hp.n_mels, nl = s->n_len;
-    if ((long)nm * nl > cap) return -nm * nl;
-    hipSetDevice(c->device);
-    // recompute n_samples from n_len: n_len = (n + 480000) / 160 is not invertible; keep it via n_len_org
-    int n_samp = 0;
-    WM_CHECK(hipMemcpy(&n_samp, s->ws.n_samp, sizeof(int), hipMemcpyDeviceToHost));
-    float* tmp;
-    WM_CHECK(hipMalloc((void**)&tmp, (size_t)nm * nl * 4));
-    launch_mel_normalize(s->ws.mel, nl, n_samp, s->ws.mel_max, nm, tmp, s->stream);
-    WM_CHECK(hipMemcpyAsync(out, tmp, (size_t)nm * nl * 4, hipMemcpyDeviceToHost, s->stream));
-    WM_CHECK(hipStreamSynchronize(s->stream));
-    WM_CHECK(hipFree(tmp));
-    return nl;
+    return guarded(nullptr, [&]() -> int {
+        if (!s || !s->ws.mel) return -1;
+        Context* c = s->ctx;
+        const int nm = c->hp.n_mels, nl = s->n_len;
+        if ((long)nm * nl > cap) return -nm * nl;
+        hipSetDevice(c->device);
+        // recompute n_samples from n_len: n_len = (n + 480000) / 160 is not invertible; keep it via n_len_org
+        int n_samp = 0;
+        WM_CHECK(hipMemcpy(&n_samp, s->ws.n_samp, sizeof(int), hipMemcpyDeviceToHost));
+        float* tmp;
+        WM_CHECK(hipMalloc((void**)&tmp, (size_t)nm * nl * 4));
+        launch_mel_normalize(s->ws.mel, nl, n_samp, s->ws.mel_max, nm, tmp, s->stream);
+        WM_CHECK(hipMemcpyAsync(out, tmp, (size_t)nm * nl * 4, hipMemcpyDeviceToHost, s->stream));
+        WM_CHECK(hipStreamSynchronize(s->stream));
+        WM_CHECK(hipFree(tmp));
+        return nl;
+    });
 }
 int whisper_mi355x_get_encoder_out(struct whisper_state* s, float* out, int cap) {
-    if (!s || !s->ws.hn || s->last_enc_windows < 1) return -1;
-    Context* c = s->ctx;
-    const long n = (long)c->hp.n_audio_ctx * c->hp.n_audio_state;
-    if (n > cap) return -1;
-    hipSetDevice(c->device);
-    std::vector<uint16_t> h(n);
-    WM_CHECK(hipMemcpy(h.data(), s->ws.hn, n * 2, hipMemcpyDeviceToHost));
-    for (long i = 0; i < n; i++) {
-        if (c->dt == DType::F16) out[i] = h2f(h[i]);
-        else { uint32_t u = (uint32_t)h[i] << 16; memcpy(&out[i], &u, 4); }
-    }
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!s || !s->ws.hn || s->last_enc_windows < 1) return -1;
+        Context* c = s->ctx;
+        const long n = (long)c->hp.n_audio_ctx * c->hp.n_audio_state;
+        if (n > cap) return -1;
+        hipSetDevice(c->device);
+        std::vector<uint16_t> h(n);
+        WM_CHECK(hipMemcpy(h.data(), s->ws.hn, n * 2, hipMemcpyDeviceToHost));
+        for (long i = 0; i < n; i++) {
+            if (c->dt == DType::F16) out[i] = h2f(h[i]);
+            else { uint32_t u = (uint32_t)h[i] << 16; memcpy(&out[i], &u, 4); }
+        }
+        return 0;
+    });
+}
+int whisper_mi355x_state_info(struct whisper_state* s, int out[5]) {
+    if (!s || !out) return -1;
+    out[0] = s->direct ? 1 : 0;
+    out[1] = s->ws.cap_jobs;
+    out[2] = s->ws.cap_cross;
+    out[3] = (int)s->dec_graphs.size();
+    out[4] = s->pooled ? 1 : 0;
+    return 5;
 }
 void* whisper_mi355x_state_stream(struct whisper_state* s) { return s ? (void*)s->stream : nullptr; }
 int whisper_mi355x_kernel_timing(struct whisper_state* s, int class_mask) {
@@ -488,138 +537,150 @@ void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
 // all device pointers; runs `reps` times and returns the average ms per launch in *ms.
 int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B, int N,
                               const float* bias, void* out, int reps, float* ms) {
-    if (!ctx) return -1;
-    hipSetDevice(ctx->c.device);
-    hipStream_t st;
-    WM_CHECK(hipStreamCreate(&st));
-    GemmArgs g{};
-    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-    g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
-    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-    if (M <= 128) {  // decode-step shapes take the split-K path, as in the engine
-        g.splitk_ws_elems = 64L * M * N;
-        WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
-    }
-    hipEvent_t e0, e1;
-    WM_CHECK(hipEventCreate(&e0));
-    WM_CHECK(hipEventCreate(&e1));
-    launch_gemm(ctx->c.dt, epi, g, st);  // warm
-    WM_CHECK(hipEventRecord(e0, st));
-    for (int r = 0; r < reps; r++) launch_gemm(ctx->c.dt, epi, g, st);
-    WM_CHECK(hipEventRecord(e1, st));
-    WM_CHECK(hipStreamSynchronize(st));
-    float t = 0;
-    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
-    if (ms) *ms = reps > 0 ? t / reps : 0.0f;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipStreamDestroy(st);
-    if (g.splitk_ws) hipFree(g.splitk_ws);
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx) return -1;
+        hipSetDevice(ctx->c.device);
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        GemmArgs g{};
+        g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        if (M <= 128) {  // decode-step shapes take the split-K path, as in the engine
+            g.splitk_ws_elems = 64L * M * N;
+            WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+        }
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        launch_gemm(ctx->c.dt, epi, g, st);  // warm
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) launch_gemm(ctx->c.dt, epi, g, st);
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        if (g.splitk_ws) hipFree(g.splitk_ws);
+        return 0;
+    });
 }
 int whisper_mi355x_debug_gemm_fp8(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale, int M,
                                   int K, const void* B8, const float* b_scale, int N, const float* bias, void* out,
                                   int reps, float* ms) {
-    if (!ctx) return -1;
-    hipSetDevice(ctx->c.device);
-    hipStream_t st;
-    WM_CHECK(hipStreamCreate(&st));
-    GemmArgs g{};
-    g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-    g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
-    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-    hipEvent_t e0, e1;
-    WM_CHECK(hipEventCreate(&e0));
-    WM_CHECK(hipEventCreate(&e1));
-    launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, st);
-    WM_CHECK(hipEventRecord(e0, st));
-    for (int r = 0; r < reps; r++) launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, st);
-    WM_CHECK(hipEventRecord(e1, st));
-    WM_CHECK(hipStreamSynchronize(st));
-    float t = 0;
-    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
-    if (ms) *ms = reps > 0 ? t / reps : 0.0f;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipStreamDestroy(st);
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx) return -1;
+        hipSetDevice(ctx->c.device);
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        GemmArgs g{};
+        g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, st);
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, st);
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        return 0;
+    });
 }
 int whisper_mi355x_debug_gemm_w8(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B8,
                                  const float* b_scale, int N, const float* bias, void* out, const float* ln_w,
                                  const float* ln_b, void* y) {
-    if (!ctx || !b_scale || M < 1 || M > 128 || K % 64) return -1;
-    hipSetDevice(ctx->c.device);
-    GemmArgs g{};
-    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-    g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
-    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-    g.w8_scale = b_scale;
-    if (epi == EPI_RESID) {
-        if (!ln_w || !y) return -1;
-        g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
-    }
-    g.splitk_ws_elems = 16L * M * N;
-    WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
-    launch_gemm(ctx->c.dt, epi, g, nullptr);
-    WM_CHECK(hipDeviceSynchronize());
-    hipFree(g.splitk_ws);
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || !b_scale || M < 1 || M > 128 || K % 64) return -1;
+        hipSetDevice(ctx->c.device);
+        GemmArgs g{};
+        g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        g.w8_scale = b_scale;
+        if (epi == EPI_RESID) {
+            if (!ln_w || !y) return -1;
+            g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
+        }
+        g.splitk_ws_elems = 16L * M * N;
+        WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+        launch_gemm(ctx->c.dt, epi, g, nullptr);
+        WM_CHECK(hipDeviceSynchronize());
+        hipFree(g.splitk_ws);
+        return 0;
+    });
 }
 int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale,
                                      void* mx_scale, int M, int K, const void* B8, const float* b_scale, int N,
                                      const float* bias, void* out) {
-    if (!ctx || !mx_scale) return -1;
-    hipSetDevice(ctx->c.device);
-    GemmArgs g{};
-    g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-    g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
-    g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-    g.mx_scale = (uint8_t*)mx_scale;
-    launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, nullptr);
-    WM_CHECK(hipDeviceSynchronize());
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || !mx_scale) return -1;
+        hipSetDevice(ctx->c.device);
+        GemmArgs g{};
+        g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        g.mx_scale = (uint8_t*)mx_scale;
+        launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, nullptr);
+        WM_CHECK(hipDeviceSynchronize());
+        return 0;
+    });
 }
 int whisper_mi355x_debug_quant_fp8(struct whisper_context* ctx, const void* x, long rows, int K, void* q, float* s) {
-    if (!ctx) return -1;
-    hipSetDevice(ctx->c.device);
-    launch_quant_rows_fp8(ctx->c.dt, x, rows, K, q, s, nullptr);
-    WM_CHECK(hipDeviceSynchronize());
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx) return -1;
+        hipSetDevice(ctx->c.device);
+        launch_quant_rows_fp8(ctx->c.dt, x, rows, K, q, s, nullptr);
+        WM_CHECK(hipDeviceSynchronize());
+        return 0;
+    });
 }
 int whisper_mi355x_debug_gemm_ln(struct whisper_context* ctx, const void* A, int M, int K, const void* B, int N,
                                  const float* bias, float* x, const float* ln_w, const float* ln_b, void* y, int reps,
                                  float* ms) {
-    if (!ctx || M > 128) return -1;
-    hipSetDevice(ctx->c.device);
-    hipStream_t st;
-    WM_CHECK(hipStreamCreate(&st));
-    GemmArgs g{};
-    g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-    g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
-    g.out = x; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-    g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-    g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
-    g.splitk_ws_elems = 64L * M * N;
-    WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
-    hipEvent_t e0, e1;
-    WM_CHECK(hipEventCreate(&e0));
-    WM_CHECK(hipEventCreate(&e1));
-    WM_CHECK(hipEventRecord(e0, st));
-    for (int r = 0; r < std::max(1, reps); r++) launch_gemm(ctx->c.dt, EPI_RESID, g, st);
-    WM_CHECK(hipEventRecord(e1, st));
-    WM_CHECK(hipStreamSynchronize(st));
-    float t = 0;
-    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
-    if (ms) *ms = t / std::max(1, reps);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipStreamDestroy(st);
-    hipFree(g.splitk_ws);
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || M > 128) return -1;
+        hipSetDevice(ctx->c.device);
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        GemmArgs g{};
+        g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = x; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        g.ln_w = ln_w; g.ln_b = ln_b; g.ln_out = y;
+        g.splitk_ws_elems = 64L * M * N;
+        WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < std::max(1, reps); r++) launch_gemm(ctx->c.dt, EPI_RESID, g, st);
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = t / std::max(1, reps);
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        hipFree(g.splitk_ws);
+        return 0;
+    });
 }
 // Direct cross attention (kernels/xattn.hip: Q' projection, one pass over E, split merge + Wv) on
 // caller data, all device pointers in the context dtype: enc [slots][n_ctx][d], slot [n] int,
@@ -627,41 +688,43 @@ int whisper_mi355x_debug_gemm_ln(struct whisper_context* ctx, const void* A, int
 int whisper_mi355x_debug_xattn(struct whisper_context* ctx, const void* enc, const int* slot, const void* q,
                                const void* wkt, const void* wv, const float* bv, int n, int n_ctx, int d, float scale,
                                int splits, float rescale_thr, void* out, int reps, float* ms) {
-    if (!ctx || n <= 0 || !xattn_supported(d)) return -1;
-    hipSetDevice(ctx->c.device);
-    const DType dt = ctx->c.dt;
-    const int H = d / 64;
-    if (splits <= 0) splits = xattn_splits(n, n_ctx);
-    void* qx = nullptr;
-    float *op = nullptr, *ml = nullptr;
-    WM_CHECK(hipMalloc(&qx, (size_t)n * 2 * H * d * 2));
-    WM_CHECK(hipMalloc((void**)&op, (size_t)n * splits * H * d * 4));
-    WM_CHECK(hipMalloc((void**)&ml, (size_t)n * splits * H * 2 * 4));
-    hipStream_t st;
-    WM_CHECK(hipStreamCreate(&st));
-    auto run = [&] {
-        launch_xattn_qproj(dt, q, wkt, n, d, H, scale, qx, st);
-        launch_xattn_step(dt, enc, slot, qx, n, n_ctx, d, splits, rescale_thr, op, ml, st);
-        launch_xattn_combine(dt, op, ml, splits, wv, bv, n, d, H, out, st);
-    };
-    hipEvent_t e0, e1;
-    WM_CHECK(hipEventCreate(&e0));
-    WM_CHECK(hipEventCreate(&e1));
-    run();
-    WM_CHECK(hipEventRecord(e0, st));
-    for (int r = 0; r < reps; r++) run();
-    WM_CHECK(hipEventRecord(e1, st));
-    WM_CHECK(hipStreamSynchronize(st));
-    float t = 0;
-    WM_CHECK(hipEventElapsedTime(&t, e0, e1));
-    if (ms) *ms = reps > 0 ? t / reps : 0.0f;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipStreamDestroy(st);
-    hipFree(qx);
-    hipFree(op);
-    hipFree(ml);
-    return 0;
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || n <= 0 || !xattn_supported(d)) return -1;
+        hipSetDevice(ctx->c.device);
+        const DType dt = ctx->c.dt;
+        const int H = d / 64;
+        if (splits <= 0) splits = xattn_splits(n, n_ctx);
+        void* qx = nullptr;
+        float *op = nullptr, *ml = nullptr;
+        WM_CHECK(hipMalloc(&qx, (size_t)n * 2 * H * d * 2));
+        WM_CHECK(hipMalloc((void**)&op, (size_t)n * splits * H * d * 4));
+        WM_CHECK(hipMalloc((void**)&ml, (size_t)n * splits * H * 2 * 4));
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        auto run = [&] {
+            launch_xattn_qproj(dt, q, wkt, n, d, H, scale, qx, st);
+            launch_xattn_step(dt, enc, slot, qx, n, n_ctx, d, splits, rescale_thr, op, ml, st);
+            launch_xattn_combine(dt, op, ml, splits, wv, bv, n, d, H, out, st);
+        };
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        run();
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) run();
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        hipFree(qx);
+        hipFree(op);
+        hipFree(ml);
+        return 0;
+    });
 }
 // ABI self-description (no device needed): sizes/offsets that a binding generator must agree on.
 int whisper_mi355x_abi_layout(size_t out[8]) {

@@ -2,18 +2,42 @@
 // vector types for 16-byte loads and MFMA fragments.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
 
-#define WM_CHECK(x)                                                                              \
-    do {                                                                                         \
-        hipError_t e_ = (x);                                                                     \
-        if (e_ != hipSuccess) {                                                                  \
-            fprintf(stderr, "whisper_mi355x: HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), \
-                    __FILE__, __LINE__, #x);                                                     \
-            abort();                                                                             \
-        }                                                                                        \
+namespace wm {
+
+// Every failure of the engine (a HIP error such as out-of-memory, an unsupported shape) is thrown
+// as wm::Error and turned into a non-zero return / NULL at the C ABI (capi.cpp), never abort():
+// whisper-rs maps a non-zero whisper_full return to WhisperError (whisper.rs:127-129) and the app's
+// streaming worker logs it and skips the chunk (state.rs:157-159).
+struct Error : std::runtime_error {
+    hipError_t hip;
+    Error(const char* m, hipError_t h) : std::runtime_error(m), hip(h) {}
+};
+[[noreturn]] __attribute__((format(printf, 2, 3))) inline void fail_hip(hipError_t h, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "whisper_mi355x: %s\n", buf);
+    throw Error(buf, h);
+}
+#define WM_FAIL(...) ::wm::fail_hip(hipSuccess, __VA_ARGS__)
+
+}  // namespace wm
+
+#define WM_CHECK(x)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            (void)hipGetLastError(); /* clear a non-sticky error (out of memory) for the next call */ \
+            ::wm::fail_hip(e_, "HIP error %s at %s:%d: %s", hipGetErrorName(e_), __FILE__, __LINE__, #x); \
+        }                                                                                             \
     } while (0)
 
 namespace wm {

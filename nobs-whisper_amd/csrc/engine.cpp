@@ -18,7 +18,22 @@ namespace wm {
 
 static size_t esize(DType) { return 2; }
 
-static void dfree(void* p) { if (p) WM_CHECK(hipFree(p)); }
+// device buffers: freed and nulled together, so that a workspace whose (re)allocation failed half way
+// can be released as a whole (ensure_ws) and the state reused
+static void dfree(void*& p) {
+    if (p) { void* q = p; p = nullptr; WM_CHECK(hipFree(q)); }
+}
+template <typename T> static void dfree(T*& p) {
+    void* q = (void*)p;
+    p = nullptr;
+    dfree(q);
+}
+template <typename T> static void dalloc(T*& p, size_t bytes) {
+    void* q = nullptr;
+    p = nullptr;
+    WM_CHECK(hipMalloc(&q, bytes));
+    p = (T*)q;
+}
 
 // ---- live kernel timing (HIP events on the state's stream) ------------------------------------------
 static hipEvent_t kt_event(whisper_state* s) {
@@ -117,43 +132,145 @@ static void tgemm(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& 
     tgemm_ws(s, cls, dt, epi, g0, st, s->ws.splitk, s->ws.splitk_elems);
 }
 
-whisper_state* new_state(Context* c) {
+static whisper_state* create_state(Context* c) {
     WM_CHECK(hipSetDevice(c->device));
     whisper_state* s = new whisper_state();
     s->ctx = c;
-    WM_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    WM_CHECK(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
-    WM_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-    WM_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    try {
+        WM_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        WM_CHECK(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
+        WM_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+        WM_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    } catch (...) {
+        if (s->ev_join) hipEventDestroy(s->ev_join);
+        if (s->ev_fork) hipEventDestroy(s->ev_fork);
+        if (s->stream2) hipStreamDestroy(s->stream2);
+        if (s->stream) hipStreamDestroy(s->stream);
+        delete s;
+        throw;
+    }
     return s;
 }
 
-static void free_ws(Workspace& w) {
-    // sub-allocations (pos/slot/.. of tok, win_seek/win_slot of win_job, pcm_ptrs/n_* of mel_ptrs)
-    // are freed with their parent
-    void* ps[] = {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, w.x, w.cross, w.self, w.dx, w.dh, w.dq, w.datt, w.dff,
-                  w.lrow, w.logits, w.probs, w.tok, w.ctl, w.tout, w.win_job, w.pcm, w.mel, w.mel_ptrs, w.splitk,
-                  w.enc, w.qx, w.xo, w.xml, w.kvslot, w.hs, w.mxs, w.qtiles};
-    for (void* p : ps) dfree(p);
-    if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
-    if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
-    if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
-    if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
-    w = Workspace();
+// A recycled state is a fresh whisper_state to its new owner: everything whisper_init_state would
+// start from (prompt_past, the rng, results, mel, timing) is reset; only the device workspace and the
+// decode graphs captured over it (keyed by active-clip count) are kept.
+static void reset_for_reuse(whisper_state* s) {
+    s->direct = false;
+    s->results.clear();
+    s->lang_ids.clear();
+    s->decisions.clear();
+    s->prompt_past.clear();
+    s->rng = std::mt19937(0);
+    s->lang_id = 0;
+    s->n_len = s->n_len_org = 0;
+    s->logits_host.clear();
+    for (double& t : s->phase_ms) t = 0;
+    s->decoded_tokens = 0;
+    s->last_enc_windows = 0;
+    s->mel_ready = false;
+    s->ktime_mask = 0;
+    for (auto& k : s->kstat) k = KStat();
+    s->cur_self_work = 0;
+    std::fill(s->ws.cross_fresh.begin(), s->ws.cross_fresh.end(), 0);
 }
 
-void free_state(whisper_state* s) {
-    if (!s) return;
+// states kept per context, and the largest workspace kept (clips): the app's pattern is one clip per
+// call (whisper.rs:83-85, state.rs:147); a batch-sized workspace is released, not kept
+static int pool_states() {
+    const char* e = getenv("WHISPER_MI355X_STATE_POOL");
+    return e ? std::max(0, atoi(e)) : 2;
+}
+static const int kPoolMaxJobs = 16;
+
+whisper_state* new_state(Context* c) {
+    {
+        std::lock_guard<std::mutex> lk(c->pool_mu);
+        if (!c->pool.empty()) {
+            whisper_state* s = c->pool.back();
+            c->pool.pop_back();
+            reset_for_reuse(s);
+            s->pooled = true;
+            return s;
+        }
+    }
+    return create_state(c);
+}
+
+static void free_ws(Workspace& w);
+
+static void destroy_state(whisper_state* s) {
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->stream);
-    drop_graphs(s);
-    free_ws(s->ws);
     hipStreamSynchronize(s->stream2);
+    drop_graphs(s);
+    try { free_ws(s->ws); } catch (const Error&) {}
+    for (auto& p : s->kpending) { hipEventDestroy(p.a); hipEventDestroy(p.b); }
+    for (hipEvent_t e : s->kpool) hipEventDestroy(e);
     hipEventDestroy(s->ev_fork);
     hipEventDestroy(s->ev_join);
     hipStreamDestroy(s->stream2);
     hipStreamDestroy(s->stream);
     delete s;
+}
+
+void free_state(whisper_state* s) {
+    if (!s) return;
+    Context* c = s->ctx;
+    hipSetDevice(c->device);
+    const bool healthy = hipStreamSynchronize(s->stream) == hipSuccess && hipStreamSynchronize(s->stream2) == hipSuccess &&
+                         s->kpending.empty();
+    if (healthy && s->ws.cap_jobs <= kPoolMaxJobs) {
+        std::lock_guard<std::mutex> lk(c->pool_mu);
+        if ((int)c->pool.size() < pool_states()) {
+            c->pool.push_back(s);
+            return;
+        }
+    }
+    destroy_state(s);
+}
+
+void drain_state_pool(Context* c) {
+    std::vector<whisper_state*> p;
+    {
+        std::lock_guard<std::mutex> lk(c->pool_mu);
+        p.swap(c->pool);
+    }
+    for (whisper_state* s : p) destroy_state(s);
+}
+
+void recover_state(whisper_state* s) {
+    if (!s) return;
+    hipSetDevice(s->ctx->device);
+    for (hipStream_t st : {s->stream, s->stream2}) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+            hipGraph_t g = nullptr;
+            hipStreamEndCapture(st, &g);
+            if (g) hipGraphDestroy(g);
+        }
+    }
+    s->capture_ev = nullptr;
+    hipStreamSynchronize(s->stream);
+    hipStreamSynchronize(s->stream2);
+    (void)hipGetLastError();
+    for (auto& p : s->kpending) { s->kpool.push_back(p.a); s->kpool.push_back(p.b); }
+    s->kpending.clear();
+}
+
+static void free_ws(Workspace& w) {
+    // sub-allocations (pos/slot/.. of tok, win_seek/win_slot of win_job, pcm_ptrs/n_* of mel_ptrs)
+    // are freed with their parent
+    dfree(w.mel_img); dfree(w.h1); dfree(w.hn); dfree(w.qkv); dfree(w.att); dfree(w.ff); dfree(w.x);
+    dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
+    dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.win_job);
+    dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.mxs); dfree(w.qtiles);
+    if (w.h_ints) hipHostFree(w.h_ints);
+    if (w.h_qtiles) hipHostFree(w.h_qtiles);
+    if (w.h_tout) hipHostFree(w.h_tout);
+    if (w.h_ctl) hipHostFree(w.h_ctl);
+    w = Workspace();
 }
 
 // prefills with at most this many tokens per clip take the direct cross attention; longer prompts
@@ -170,16 +287,12 @@ static const float kXattnThr = 8.0f;
 // forces a form; otherwise direct above WHISPER_MI355X_CROSS_CACHE_MAX (default 32) clips.
 static bool pick_direct(Context* c, int n_jobs) {
     if (!c->cross_direct) return false;
-    static const int mode = [] {
-        const char* e = getenv("WHISPER_MI355X_CROSS");
-        return !e ? 0 : strcmp(e, "direct") == 0 ? 1 : strcmp(e, "cache") == 0 ? 2 : 0;
-    }();
-    static const int cache_max = [] {
-        const char* e = getenv("WHISPER_MI355X_CROSS_CACHE_MAX");
-        return e ? atoi(e) : 32;
-    }();
-    if (mode) return mode == 1;
-    return n_jobs > cache_max;
+    // read per call (tests switch the form per case)
+    const char* e = getenv("WHISPER_MI355X_CROSS");
+    if (e && strcmp(e, "direct") == 0) return true;
+    if (e && strcmp(e, "cache") == 0) return false;
+    const char* m = getenv("WHISPER_MI355X_CROSS_CACHE_MAX");
+    return n_jobs > (m ? atoi(m) : 32);
 }
 
 static int enc_batch_cap() {
@@ -188,33 +301,45 @@ static int enc_batch_cap() {
     return v > 0 ? v : 32;
 }
 
+// Cross K/V cache for at least `slots` slots (cache form: the call's clips; direct form: the clips
+// whose prompts are too long for the direct prefill). Sized by the calls that use it, so a state
+// that ran a large direct-form batch does not allocate a cache for all of its slots later.
+static void ensure_cross(Context* c, Workspace& w, int slots) {
+    if (w.cross && w.cap_cross >= slots) return;
+    const Hparams& hp = c->hp;
+    dfree(w.cross);
+    w.cap_cross = 0;
+    std::fill(w.cross_fresh.begin(), w.cross_fresh.end(), 0);
+    dalloc(w.cross, (size_t)slots * hp.n_text_layer * 2 * hp.n_audio_ctx * hp.n_audio_state * esize(c->dt));
+    w.cap_cross = slots;
+}
+
 // (Re)allocate the workspace for n_jobs clips. Encoder activations are sized for at most
-// enc_batch_cap() windows at once; caches for n_jobs slots.
-static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
+// enc_batch_cap() windows at once; caches for n_jobs slots. If an allocation fails (out of memory),
+// the whole workspace is released and the error propagates: the state stays usable (empty).
+static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
     Workspace& w = s->ws;
     const Hparams& hp = c->hp;
     const size_t d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, E = esize(c->dt);
     const int n_enc = std::min(n_jobs, enc_batch_cap());
-    size_t unused = 0;
     if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
-        for (void* p : {w.mel_img, w.h1, w.hn, w.qkv, w.att, w.ff, (void*)w.x, (void*)w.win_job, (void*)w.hs, (void*)w.mxs})
-            dfree(p);
-        w.hs = nullptr;
-        w.mxs = nullptr;
-        WM_CHECK(hipMalloc(&w.mel_img, (size_t)n_enc * 3002 * nm * E));
-        WM_CHECK(hipMalloc(&w.h1, (size_t)n_enc * 3002 * d * E));
+        dfree(w.mel_img); dfree(w.h1); dfree(w.hn); dfree(w.qkv); dfree(w.att); dfree(w.ff); dfree(w.x);
+        dfree(w.win_job); dfree(w.hs); dfree(w.mxs);
+        w.cap_enc = 0;
+        dalloc(w.mel_img, (size_t)n_enc * 3002 * nm * E);
+        dalloc(w.h1, (size_t)n_enc * 3002 * d * E);
         WM_CHECK(hipMemset(w.h1, 0, (size_t)n_enc * 3002 * d * E));  // conv padding rows stay zero
-        WM_CHECK(hipMalloc(&w.hn, (size_t)n_enc * T * d * E));
-        WM_CHECK(hipMalloc(&w.qkv, (size_t)n_enc * T * 3 * d * E));
-        WM_CHECK(hipMalloc(&w.att, (size_t)n_enc * T * d * E));
-        WM_CHECK(hipMalloc(&w.ff, (size_t)n_enc * T * 4 * d * E));
-        WM_CHECK(hipMalloc((void**)&w.x, (size_t)n_enc * T * d * 4));
+        dalloc(w.hn, (size_t)n_enc * T * d * E);
+        dalloc(w.qkv, (size_t)n_enc * T * 3 * d * E);
+        dalloc(w.att, (size_t)n_enc * T * d * E);
+        dalloc(w.ff, (size_t)n_enc * T * 4 * d * E);
+        dalloc(w.x, (size_t)n_enc * T * d * 4);
         if (c->fp8_enc) {
-            WM_CHECK(hipMalloc((void**)&w.hs, (size_t)n_enc * T * sizeof(float)));
-            WM_CHECK(hipMalloc((void**)&w.mxs, (size_t)n_enc * T * (4 * d / 32)));
+            dalloc(w.hs, (size_t)n_enc * T * sizeof(float));
+            dalloc(w.mxs, (size_t)n_enc * T * (4 * d / 32));
         }
-        WM_CHECK(hipMalloc((void**)&w.win_job, (size_t)n_enc * 3 * sizeof(int)));
+        dalloc(w.win_job, (size_t)n_enc * 3 * sizeof(int));
         w.win_seek = w.win_job + n_enc;
         w.win_slot = w.win_job + 2 * n_enc;
         w.cap_enc = n_enc;
@@ -222,71 +347,79 @@ static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
     if (n_jobs > w.cap_jobs) {
         const int L = hp.n_text_layer;
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
-        for (void* p : {w.cross, w.self, (void*)w.dx, w.dh, w.dq, w.datt, w.dff, w.lrow, (void*)w.logits, (void*)w.probs,
-                        (void*)w.tok, (void*)w.ctl, (void*)w.tout, (void*)w.mel_ptrs, (void*)w.splitk, w.enc, w.qx,
-                        (void*)w.xo, (void*)w.xml, (void*)w.kvslot, (void*)w.qtiles})
-            dfree(p);
-        if (w.h_qtiles) WM_CHECK(hipHostFree(w.h_qtiles));
-        w.cross = w.enc = w.qx = nullptr;
-        w.xo = w.xml = nullptr;
-        w.cap_xq = 0;
-        w.splitk_elems = 16L * std::min(n_tok, 256) * 4 * (long)d;
-        WM_CHECK(hipMalloc((void**)&w.splitk, w.splitk_elems * 4));
-        if (w.h_ints) WM_CHECK(hipHostFree(w.h_ints));
-        if (w.h_tout) WM_CHECK(hipHostFree(w.h_tout));
-        if (w.h_ctl) WM_CHECK(hipHostFree(w.h_ctl));
+        dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
+        dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.mel_ptrs);
+        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles);
+        for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
+            if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
+        w.cap_jobs = w.cap_tok = w.cap_cross = w.cap_xq = 0;
+        // split-K slabs: decode steps (<= 128 rows per group, two concurrent groups) and the prefill
+        // GEMMs below the big-GEMM size (M*N < 2^22), whose split count depends on N and K only
+        // (kernels/gemm.hip dec_splits_for: splits * N <= 16384, <= 12 splits)
+        w.splitk_elems = std::max(16L * std::min(n_tok, 256) * 4 * (long)d, std::min(16384L * n_tok, 12L << 22));
+        dalloc(w.splitk, w.splitk_elems * 4);
         w.cross_fresh.assign(n_jobs, 0);
         {
             std::vector<int> ident(n_jobs);
             for (int k = 0; k < n_jobs; k++) ident[k] = k;
-            WM_CHECK(hipMalloc((void**)&w.kvslot, (size_t)n_jobs * sizeof(int)));
+            dalloc(w.kvslot, (size_t)n_jobs * sizeof(int));
             WM_CHECK(hipMemcpy(w.kvslot, ident.data(), (size_t)n_jobs * sizeof(int), hipMemcpyHostToDevice));
         }
-        WM_CHECK(hipMalloc(&w.self, (size_t)n_jobs * L * 2 * hp.n_text_ctx * d * E));
-        WM_CHECK(hipMalloc((void**)&w.dx, (size_t)n_tok * d * 4));
-        WM_CHECK(hipMalloc(&w.dh, (size_t)n_tok * d * E));
-        WM_CHECK(hipMalloc(&w.dq, (size_t)n_tok * d * E));
-        WM_CHECK(hipMalloc(&w.datt, (size_t)n_tok * d * E));
-        WM_CHECK(hipMalloc(&w.dff, (size_t)n_tok * 4 * d * E));
-        WM_CHECK(hipMalloc(&w.lrow, (size_t)n_jobs * d * E));
-        WM_CHECK(hipMalloc((void**)&w.logits, (size_t)n_jobs * hp.n_vocab * 4));
-        WM_CHECK(hipMalloc((void**)&w.probs, (size_t)n_jobs * 2 * hp.n_vocab * 4));
-        WM_CHECK(hipMalloc((void**)&w.tok, ((size_t)5 * n_tok + n_jobs) * sizeof(int)));
+        dalloc(w.self, (size_t)n_jobs * L * 2 * hp.n_text_ctx * d * E);
+        dalloc(w.dx, (size_t)n_tok * d * 4);
+        dalloc(w.dh, (size_t)n_tok * d * E);
+        dalloc(w.dq, (size_t)n_tok * d * E);
+        dalloc(w.datt, (size_t)n_tok * d * E);
+        dalloc(w.dff, (size_t)n_tok * 4 * d * E);
+        dalloc(w.lrow, (size_t)n_jobs * d * E);
+        dalloc(w.logits, (size_t)n_jobs * hp.n_vocab * 4);
+        dalloc(w.probs, (size_t)n_jobs * 2 * hp.n_vocab * 4);
+        dalloc(w.tok, ((size_t)5 * n_tok + n_jobs) * sizeof(int));
         w.pos = w.tok + n_tok;
         w.slot = w.tok + 2 * n_tok;
         w.nkv_self = w.tok + 3 * n_tok;
         w.nkv_cross = w.tok + 4 * n_tok;
         w.lrows = w.tok + 5 * n_tok;
-        WM_CHECK(hipMalloc((void**)&w.ctl, (size_t)n_jobs * sizeof(SeqCtl)));
-        WM_CHECK(hipMalloc((void**)&w.tout, (size_t)n_jobs * sizeof(TokOut)));
-        WM_CHECK(hipMalloc((void**)&w.mel_ptrs, (size_t)n_jobs * (2 * sizeof(void*) + 3 * sizeof(int))));
+        dalloc(w.ctl, (size_t)n_jobs * sizeof(SeqCtl));
+        dalloc(w.tout, (size_t)n_jobs * sizeof(TokOut));
+        dalloc(w.mel_ptrs, (size_t)n_jobs * (2 * sizeof(void*) + 3 * sizeof(int)));
         w.pcm_ptrs = (const float**)(w.mel_ptrs + n_jobs);
         w.n_samp = (int*)(w.pcm_ptrs + n_jobs);
         w.n_len = w.n_samp + n_jobs;
         w.mel_max = w.n_len + n_jobs;
         WM_CHECK(hipHostMalloc((void**)&w.h_ints, ((size_t)5 * n_tok + n_jobs) * sizeof(int) + 64, 0));
-        WM_CHECK(hipMalloc((void**)&w.qtiles, (size_t)n_tok * sizeof(int2)));
+        dalloc(w.qtiles, (size_t)n_tok * sizeof(int2));
         WM_CHECK(hipHostMalloc((void**)&w.h_qtiles, (size_t)n_tok * sizeof(int2), 0));
         WM_CHECK(hipHostMalloc((void**)&w.h_tout, (size_t)n_jobs * sizeof(TokOut), 0));
         WM_CHECK(hipHostMalloc((void**)&w.h_ctl, (size_t)n_jobs * sizeof(SeqCtl), 0));
         w.cap_jobs = n_jobs;
         w.cap_tok = n_tok;
     }
-    (void)unused;
     // the buffers of this call's cross attention form (allocated on first use, kept)
     if (s->direct && !w.enc) {
         // no cross K/V cache up front: decode steps (and short prefills) read E directly
         const int H = hp.n_text_head;
         w.cap_xq = std::max(kXDirectMaxTok * w.cap_jobs, 128);
-        // n * xattn_splits(n) <= max(n, 255 + n); two decode row groups at most double that
+        // n * xattn_splits(n) <= max(n, 255 + n) per row group; two concurrent groups at most double it
         const size_t xo_rows = (size_t)std::max(w.cap_xq, 512) + w.cap_jobs + 512;
-        WM_CHECK(hipMalloc(&w.enc, (size_t)w.cap_jobs * T * d * E));
-        WM_CHECK(hipMalloc(&w.qx, (size_t)w.cap_xq * 2 * H * d * E));
-        WM_CHECK(hipMalloc((void**)&w.xo, xo_rows * H * d * 4));
-        WM_CHECK(hipMalloc((void**)&w.xml, xo_rows * H * 2 * 4));
+        dalloc(w.enc, (size_t)w.cap_jobs * T * d * E);
+        dalloc(w.qx, (size_t)w.cap_xq * 2 * H * d * E);
+        dalloc(w.xo, xo_rows * H * d * 4);
+        dalloc(w.xml, xo_rows * H * 2 * 4);
     }
-    if (!s->direct && !w.cross)
-        WM_CHECK(hipMalloc(&w.cross, (size_t)w.cap_jobs * hp.n_text_layer * 2 * T * d * E));
+    if (!s->direct) ensure_cross(c, w, n_jobs);
+}
+
+static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
+    try {
+        ensure_ws_impl(c, s, n_jobs);
+    } catch (const Error&) {
+        hipStreamSynchronize(s->stream);
+        hipStreamSynchronize(s->stream2);
+        drop_graphs(s);
+        free_ws(s->ws);
+        throw;
+    }
 }
 
 // ---- mel ------------------------------------------------------------------------------------------
@@ -307,12 +440,14 @@ int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int
     }
     if (!on_device && pcm_tot > w.cap_pcm) {
         dfree(w.pcm);
-        WM_CHECK(hipMalloc((void**)&w.pcm, pcm_tot * 4));
+        w.cap_pcm = 0;
+        dalloc(w.pcm, pcm_tot * 4);
         w.cap_pcm = pcm_tot;
     }
     if (mel_tot > w.cap_mel) {
         dfree(w.mel);
-        WM_CHECK(hipMalloc((void**)&w.mel, mel_tot * 4));
+        w.cap_mel = 0;
+        dalloc(w.mel, mel_tot * 4);
         w.cap_mel = mel_tot;
     }
     std::vector<const float*> pp(n_jobs);
@@ -348,6 +483,7 @@ int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int
     WM_CHECK(hipStreamSynchronize(s->stream));  // blk (pageable) must outlive the copy
     s->n_len = mel_n_len(n[0]);
     s->n_len_org = mel_n_len_org(n[0]);
+    s->mel_ready = true;
     return 0;
 }
 
@@ -383,7 +519,7 @@ static void ensure_fp8(Context* c) {
     const size_t t = hp.n_text_state, nd = dec_fp8() ? hp.n_text_layer : 0;
     const size_t per_d = 14 * t * t, per_ds = (3 * t + 3 * t + 4 * t + t) * sizeof(float);
     WM_CHECK(hipSetDevice(c->device));
-    WM_CHECK(hipMalloc((void**)&c->arena8, nl * (per + per_s) + nd * (per_d + per_ds)));
+    dalloc(c->arena8, nl * (per + per_s) + nd * (per_d + per_ds));
     c->enc8.assign(nl, Context::Fp8Layer{});
     char* p = c->arena8;
     for (size_t l = 0; l < nl; l++) {
@@ -567,6 +703,17 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, 
     WM_CHECK(hipMemcpyAsync(w.qtiles, w.h_qtiles, (size_t)nt * sizeof(int2), hipMemcpyHostToDevice, s->stream));
 }
 
+// WHISPER_MI355X_XSERP=1: odd decoder layers read each clip's encoder rows in reverse order, so that
+// the rows a workgroup read last in layer l (still in the 256 MB die-level cache) are read first in
+// layer l + 1 (A/B experiment)
+static bool xattn_serp() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_XSERP");
+        return e && atoi(e) == 1;
+    }();
+    return on;
+}
+
 // One group of decoder rows on one stream: rows [r0, r0+n) of the token arrays and activations,
 // with its own split-K slab region and cross-attention partials, so that two groups can run at the
 // same time (decode steps).
@@ -633,7 +780,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         g.splitk_ws_elems = v.splitk_elems;
         KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
         const int splits = launch_gemm_partials(dt, g, st);
-        if (splits <= 0) { fprintf(stderr, "whisper_mi355x: decode partials GEMM not applicable\n"); abort(); }
+        if (splits <= 0) WM_FAIL("decode partials GEMM not applicable");
         return DecSlabs{v.splitk, splits, (long)n_tok * N, N, bias, scale};
     };
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
@@ -672,7 +819,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             {
                 // the roofline class holds decode steps only (E bytes read once per clip and layer)
                 KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2, st, kt_layer);
-                launch_xattn_step(dt, w.enc, slot, qx, n_tok, Ta, d, S, kXattnThr, v.xo, v.xml, st);
+                launch_xattn_step(dt, w.enc, slot, qx, n_tok, Ta, d, S, kXattnThr, v.xo, v.xml, st, xattn_serp() ? (l & 1) : 0);
             }
             {
                 KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d, st);
@@ -704,34 +851,46 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     }
 }
 
-// WHISPER_MI355X_DEC_STREAMS=2: decode steps of >= 32 clips run as two row groups, one per stream,
-// forked from and joined back into the state's stream (two independent branches of the step's
-// hipGraph), so that each group's chain of small latency-bound launches could overlap the other's.
-// Off by default: measured slower on large-v3 at 128 clips (2360-2392 vs 2729-2740 audio-s/s;
-// the cross-attention pass at 64 clips per group reads E at 3.6 instead of 4.7 TB/s).
-// Above 128 clips a step does not fit one fused pass (<= 128 rows), so it runs as two fused groups
-// by default (measured the same as the unfused path in bf16: decode 213 vs 217 ms per step on turbo
-// at 256 clips; the fp8 decoder weights exist only on the fused path).
+// Row groups of a decode step. The fused pass (every LayerNorm folded into a split-K reduce) takes at
+// most 128 rows, so a step over n > 128 clips runs as ceil(n / 128) fused groups of near-equal size,
+// alternating between the state's two streams (forked from and joined back into the state's stream:
+// branches of the step's hipGraph); two groups for 129..256 clips measured the same as the unfused
+// path in bf16 (turbo at 256 clips: decode 213 vs 217 ms per step) and the fp8 decoder weights exist
+// only on the fused path.
+// WHISPER_MI355X_DEC_STREAMS=2: also split steps of 32..128 clips into two concurrent groups. Off by
+// default: measured slower on large-v3 at 128 clips (2360-2392 vs 2729-2740 audio-s/s; the
+// cross-attention pass at 64 clips per group reads E at 3.6 instead of 4.7 TB/s).
 static int dec_groups(int n_tok) {
     static const int g = [] {
         const char* e = getenv("WHISPER_MI355X_DEC_STREAMS");
         return e ? atoi(e) : 0;
     }();
-    if (g == 0) return n_tok > 128 && n_tok <= 256 ? 2 : 1;
-    return (g >= 2 && n_tok >= 32) ? 2 : 1;
+    const int need = cdiv(n_tok, 128);
+    if (g >= 2 && n_tok >= 32) return std::max(2, need);
+    return need;
 }
 
-// the two row groups of a decode step: rows [0, na) on the state's stream, [na, n) on stream2, each
-// with its own half of the split-K slabs and its own cross-attention partials
-static void dec_views(Context* c, whisper_state* s, int n_tok, bool xdirect, DecView& a, DecView& b) {
+// The two stream halves of a decode step's scratch: group views on the state's stream use the first
+// half of the split-K slabs and cross-attention partials, views on stream2 the second. A group of
+// <= gmax rows uses at most gmax * xattn_splits(gmax) partial rows.
+static void dec_halves(Context* c, whisper_state* s, int gmax, bool xdirect, DecView& a, DecView& b) {
     Workspace& w = s->ws;
     const int H = c->hp.n_text_head, d = c->hp.n_text_state;
-    const int na = (n_tok + 1) / 2, nb = n_tok - na;
     const long half = w.splitk_elems / 2;
-    const long xoff = xdirect ? (long)na * xattn_splits(na, c->hp.n_audio_ctx) : 0;
-    a = DecView{0, na, s->stream, w.splitk, half, w.xo, w.xml};
-    b = DecView{na, nb, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
+    long xoff = 0;
+    if (xdirect)
+        for (int n = 1; n <= gmax; n++) xoff = std::max(xoff, (long)n * xattn_splits(n, c->hp.n_audio_ctx));
+    a = DecView{0, 0, s->stream, w.splitk, half, w.xo, w.xml};
+    b = DecView{0, 0, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
                 w.xml ? w.xml + xoff * H * 2 : nullptr};
+}
+
+// the two row groups of a decode step: rows [0, na) on the state's stream, [na, n) on stream2
+static void dec_views(Context* c, whisper_state* s, int n_tok, bool xdirect, DecView& a, DecView& b) {
+    const int na = (n_tok + 1) / 2, nb = n_tok - na;
+    dec_halves(c, s, na, xdirect, a, b);
+    a.r0 = 0; a.n = na;
+    b.r0 = na; b.n = nb;
 }
 
 // WHISPER_MI355X_DEC_GRAPHS2=1: the two row groups as two separate hipGraphs launched on two streams
@@ -746,20 +905,26 @@ static bool dec_two_graphs() {
 
 static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
     Workspace& w = s->ws;
-    const int groups = rows_identity && n_rows == n_tok ? dec_groups(n_tok) : 1;
-    const bool fused = rows_identity && n_rows == n_tok && cdiv(n_tok, groups) <= 128;
-    if (groups == 1 || !fused) {
+    const bool step = rows_identity && n_rows == n_tok;  // a decode step: one token per clip, logits of every row
+    const int groups = step ? dec_groups(n_tok) : 1;
+    if (groups == 1) {
+        // prefill / language detection / whisper_decode: the unfused pass over the tiles that
+        // decoder_upload built (decoder_forward); decode steps of <= 128 clips: one fused pass
         const DecView v{0, n_tok, s->stream, w.splitk, w.splitk_elems, w.xo, w.xml};
-        decoder_rows(c, s, v, n_rows, fused, xdirect, 1.0);
+        decoder_rows(c, s, v, n_rows, step, xdirect, 1.0);
         return;
     }
-    DecView a, b;
-    dec_views(c, s, n_tok, xdirect, a, b);
-    const int na = a.n, nb = b.n;
+    const int gsz = cdiv(n_tok, groups);
+    DecView half[2];
+    dec_halves(c, s, gsz, xdirect, half[0], half[1]);
     WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
     WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
-    decoder_rows(c, s, a, na, true, xdirect, (double)na / n_tok);
-    decoder_rows(c, s, b, nb, true, xdirect, (double)nb / n_tok);
+    for (int g = 0, r0 = 0; r0 < n_tok; g++, r0 += gsz) {
+        DecView v = half[g & 1];
+        v.r0 = r0;
+        v.n = std::min(gsz, n_tok - r0);
+        decoder_rows(c, s, v, v.n, true, xdirect, (double)v.n / n_tok);
+    }
     WM_CHECK(hipEventRecord(s->ev_join, s->stream2));
     WM_CHECK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
 }
@@ -772,8 +937,10 @@ static void ensure_cross_cache(Context* c, whisper_state* s, const std::vector<i
     const Hparams& hp = c->hp;
     const int d = hp.n_audio_state, T = hp.n_audio_ctx, L = hp.n_text_layer;
     const size_t E = esize(c->dt);
-    if (!w.cross) WM_CHECK(hipMalloc(&w.cross, (size_t)w.cap_jobs * L * 2 * T * d * E));
     std::vector<int> stale;
+    int need = 0;
+    for (int sl : slots) need = std::max(need, sl + 1);
+    ensure_cross(c, w, need);
     for (int sl : slots)
         if (!w.cross_fresh[sl]) stale.push_back(sl);
     std::sort(stale.begin(), stale.end());

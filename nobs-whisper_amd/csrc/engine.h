@@ -97,6 +97,11 @@ struct Context {
     // (logits), the cross-attention K/V weights and prefill keep the compute type
     struct Fp8Dec { void *wqkv, *wo, *wxq, *wxo, *w1, *w2; float *sqkv, *so, *sxq, *sxo, *s1, *s2; };
     std::vector<Fp8Dec> dec8;
+    // States released by whisper_free_state, kept with their workspace and captured decode graphs
+    // for the next whisper_init_state: whisper.rs:83-85 creates (and drops) a state on every
+    // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.
+    std::mutex pool_mu;
+    std::vector<whisper_state*> pool;
 };
 
 struct TokenData {
@@ -114,6 +119,7 @@ struct Segment {
 // Workspace sized for a batch of up to `cap_jobs` clips; grows on demand, never shrinks.
 struct Workspace {
     int cap_jobs = 0, cap_enc = 0, cap_tok = 0;
+    int cap_cross = 0;  // slots of the cross K/V cache (sized by the calls that use it, not cap_jobs)
     size_t cap_mel = 0, cap_pcm = 0;
     // encoder (cap_enc windows)
     void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
@@ -187,6 +193,8 @@ struct whisper_state {
     long decoded_tokens = 0;
     // standalone encode/decode API support
     int last_enc_windows = 0;
+    bool mel_ready = false;  // whisper_pcm_to_mel (or a full call) has run on this state
+    bool pooled = false;     // this state was recycled from the context's pool (workspace + graphs kept)
     // kernel timing (off unless whisper_mi355x_kernel_timing enabled it)
     int ktime_mask = 0;  // bit k: time kernel class k
     wm::KStat kstat[wm::K_NCLASS];
@@ -209,6 +217,11 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
 void free_context(Context* c);
 whisper_state* new_state(Context* c);
 void free_state(whisper_state* s);
+// after an engine error (wm::Error) mid-call: end a half-done graph capture, drain both streams and
+// return pending timing events, so that the state and its context stay usable
+void recover_state(whisper_state* s);
+// frees the states kept in the context's pool (whisper_free)
+void drain_state_pool(Context* c);
 
 struct FullOpts {
     int fixed_tokens = 0;

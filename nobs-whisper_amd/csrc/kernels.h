@@ -126,8 +126,9 @@ bool xattn_supported(int d);
 int xattn_splits(int n, int Tn);
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st);
+// rev = 1: each split's 16-row tiles in reverse order (the engine alternates per decoder layer)
 void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
-                       float thr, float* opart, float* ml, hipStream_t st);
+                       float thr, float* opart, float* ml, hipStream_t st, int rev = 0);
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st);
 

@@ -784,7 +784,7 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv, int n,
                         int L, int layer, int H, int ctx, int d, void* out, int kind, hipStream_t st) {
     if (n <= 0) return;
-    if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
+    if (ctx > 1536) WM_FAIL("attention context %d > 1536", ctx);
     dim3 grid(n, H);
 #define WM_ATTN_DEC(TT, KN) \
     KN<TT><<<grid, 256, 0, st>>>((const TT*)q, q_stride, (const TT*)cache, slot, n_kv, L, layer, H, ctx, d, (TT*)out)
@@ -801,7 +801,7 @@ void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache
 void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
                             int L, int layer, int H, int ctx, int d, void* out, hipStream_t st) {
     if (n <= 0) return;
-    if (ctx > 1536) { fprintf(stderr, "whisper_mi355x: attention context %d > 1536\n", ctx); abort(); }
+    if (ctx > 1536) WM_FAIL("attention context %d > 1536", ctx);
     dim3 grid(n, H);
     if (dt == DType::F16)
         attn_cross_step_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)cache, slot, n_kv, L, layer, H, ctx, d, (half_t*)out);
@@ -812,7 +812,7 @@ void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, con
 void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int* slot, const int* pos, int n, int L,
                            int layer, int H, int ctx, int d, void* out, hipStream_t st) {
     if (n <= 0) return;
-    if (ctx > 448) { fprintf(stderr, "whisper_mi355x: self-attention context %d > 448\n", ctx); abort(); }
+    if (ctx > 448) WM_FAIL("self-attention context %d > 448", ctx);
     const int hpb = H % 4 == 0 ? 4 : H % 2 == 0 ? 2 : 1;
     // non-temporal K/V reads with WHISPER_MI355X_SELF_NT=1 (A/B: 3048-3053 vs 3050-3057 audio-s/s
     // with the default policy, so off)

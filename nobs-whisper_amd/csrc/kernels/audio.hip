@@ -123,13 +123,13 @@ void launch_silence_boundaries(const float* const* pcm, const int* n_samples, in
                                hipStream_t st) {
     if (n_clips <= 0) return;
     const int ws = sample_rate / 50;
-    if (ws <= 0) { fprintf(stderr, "whisper_mi355x: sample rate %d too low for 20 ms windows\n", sample_rate); abort(); }
+    if (ws <= 0) WM_FAIL("sample rate %d too low for 20 ms windows", sample_rate);
     const int max_win = max_n / ws;
-    if (max_win > rms_stride) { fprintf(stderr, "whisper_mi355x: rms row %d < %d windows\n", rms_stride, max_win); abort(); }
+    if (max_win > rms_stride) WM_FAIL("rms row %d < %d windows", rms_stride, max_win);
     if (max_win > 0) {
         const int wpg = std::max(1, std::min(64, (int)((120 * 1024) / ((ws + 1) * 4))));
         const size_t lds = (size_t)wpg * (ws + 1) * 4;
-        if (lds > 160 * 1024) { fprintf(stderr, "whisper_mi355x: 20 ms window of %d samples too large\n", ws); abort(); }
+        if (lds > 160 * 1024) WM_FAIL("20 ms window of %d samples too large", ws);
         rms_windows_kernel<<<dim3((max_win + wpg - 1) / wpg, n_clips), RMS_THREADS, lds, st>>>(pcm, n_samples, ws, wpg,
                                                                                              rms, rms_stride);
     }
@@ -199,7 +199,7 @@ resample_kernel(const float* const* __restrict__ in, const int* __restrict__ n_i
 void launch_resample(const float* const* in, const int* n_in, int n_clips, int max_out, const float* W, int ldw, int fsi,
                      int fso, float* const* out, const int* n_out, hipStream_t st) {
     if (n_clips <= 0 || max_out <= 0) return;
-    if (ldw % RS_BN || ldw < fso) { fprintf(stderr, "whisper_mi355x: resampler operator stride %d\n", ldw); abort(); }
+    if (ldw % RS_BN || ldw < fso) WM_FAIL("resampler operator stride %d", ldw);
     const int rows = (max_out + fso - 1) / fso;
     const int col_tiles = ldw / RS_BN;
     const int row_tiles = (rows + RS_BM - 1) / RS_BM;

@@ -1081,6 +1081,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each 64 rows x 32 columns
     const int n0 = blockIdx.x * BN;
+    const int m0 = blockIdx.y * BM;  // row chunk (prefill: M > 128 as chunks of 128 rows, same math per row)
     const int k0 = SPLIT ? blockIdx.z * kc : 0;
     const int nkt = min(kc, g.K - k0) / BK;
     const T* A = (const T*)g.A;
@@ -1093,7 +1094,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
     for (int i = 0; i < 4; i++) {
         const int r = (wave * 4 + i) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
-        const int m = min(r, g.M - 1);
+        const int m = min(m0 + r, g.M - 1);
         a_src[i] = A + (long)m * g.a_rstride + k0 + c * 8;
     }
     if constexpr (W8) {  // one piece per wave: 16 rows x 4 chunks; LDS slot p = row*4 + phys chunk
@@ -1199,7 +1200,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
             const float wsc = W8 ? g.w8_scale[n] : 1.0f;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
                 if (m >= g.M) continue;
                 const float v = W8 ? acc[i][j][r] * wsc : acc[i][j][r];
                 if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = v;
@@ -1383,7 +1384,7 @@ static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st
     const int npt = cdiv(g.N, 256);
     if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
     else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
-    else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+    else WM_FAIL("fused LN width %d > 2048", g.N);
 }
 
 // big-GEMM tile order: 0 = row-major over (m-tile, n-tile) after the XCD remap; > 0 = groups of this
@@ -1400,10 +1401,7 @@ template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     if (g.w8_scale) {  // e4m3 weights: the decode-step split-K kernel only
         const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
-        if (!(g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0 && (EPI != EPI_RESID || fused_ln))) {
-            fprintf(stderr, "whisper_mi355x: e4m3 weights need the decode-step GEMM path (M %d <= 128, K %% 64 == 0)\n", g.M);
-            abort();
-        }
+        if (!(g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0 && (EPI != EPI_RESID || fused_ln))) WM_FAIL("e4m3 weights need the decode-step GEMM path (M %d <= 128, K %% 64 == 0)", g.M);
     }
     const bool big256 = g_gemm_variant >= 2 ||
                         (g_gemm_variant < 0 && (g.N % 256 == 0 || g.N >= 1024) && g.M >= 1024);
@@ -1426,33 +1424,32 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
     }
     const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
     const int nk = cdiv(g.K, 64);
-    if (g.splitk_ws && g.M <= 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
-        // decode step (gemm_dec_kernel): split K until the grid has >= 160 workgroups, chunks of
-        // >= 2 K-tiles and <= 8 splits (the reduce reads splits x M x N f32). (Chunks of >= 5
-        // K-tiles measured faster in isolation, 9.6 vs 10.4 us at N = K = 1280, but not in the
-        // decode step: 82.0 vs 81.6 us of GEMM + reduce per layer.)
+    if (g.splitk_ws && (g.M <= 128 || !fused_ln) && g.K % 64 == 0 && g_gemm_variant != 0) {
+        // decode step and small prefill (gemm_dec_kernel; M > 128 as 128-row chunks, gridDim.y): the
+        // split count depends on N and K only (dec_splits_for), so a row's sums, and the bits of every
+        // result, do not depend on how many clips share the launch (batch == single). (Chunks of >= 5
+        // K-tiles measured faster in isolation, 9.6 vs 10.4 us at N = K = 1280, but not in the decode
+        // step: 82.0 vs 81.6 us of GEMM + reduce per layer.)
         const int tiles = cdiv(g.N, 64);
+        const int mch = cdiv(g.M, 128);
         int splits = dec_splits_for(tiles, nk);
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
         const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64 && !g.w8_scale;
-        if (g.w8_scale && (long)splits * g.M * g.N > g.splitk_ws_elems) {
-            fprintf(stderr, "whisper_mi355x: e4m3 decode GEMM: split-K workspace too small\n");
-            abort();
-        }
+        if (g.w8_scale && (long)splits * g.M * g.N > g.splitk_ws_elems) WM_FAIL("e4m3 decode GEMM: split-K workspace too small");
         if ((long)splits * g.M * g.N <= g.splitk_ws_elems && !small_unsplit) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
-                if (g.w8_scale) gemm_dec_kernel<T, EPI, false, 2, true><<<tiles, 256, 0, st>>>(g, kc);
-                else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<tiles, 256, 0, st>>>(g, kc);
-                else gemm_dec_kernel<T, EPI, false><<<tiles, 256, 0, st>>>(g, kc);
+                if (g.w8_scale) gemm_dec_kernel<T, EPI, false, 2, true><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
+                else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
+                else gemm_dec_kernel<T, EPI, false><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
                 return;
             }
-            if (g.w8_scale) gemm_dec_kernel<T, EPI, true, 2, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
-            else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
-            else gemm_dec_kernel<T, EPI, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+            if (g.w8_scale) gemm_dec_kernel<T, EPI, true, 2, true><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
+            else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
+            else gemm_dec_kernel<T, EPI, true><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
             } else {
@@ -1479,7 +1476,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
                 const int npt = cdiv(g.N, 256);
                 if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
                 else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
-                else { fprintf(stderr, "whisper_mi355x: fused LN width %d > 2048\n", g.N); abort(); }
+                else WM_FAIL("fused LN width %d > 2048", g.N);
             } else {
                 const long total = (long)g.M * g.N;
                 splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
@@ -1491,7 +1488,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         }
         return;
     }
-    if (fused_ln) { fprintf(stderr, "whisper_mi355x: fused LN requires the decode split-K path\n"); abort(); }
+    if (fused_ln) WM_FAIL("fused LN requires the decode split-K path");
     const int tiles = cdiv(g.N, 64) * cdiv(g.M, 64);
     int splits = std::min(16, std::max(1, 512 / tiles));
     splits = std::min(splits, std::max(1, nk / 2));
@@ -1519,7 +1516,7 @@ static void launch_dt(int epi, const GemmArgs& g, hipStream_t st) {
         case EPI_F32: launch_t<T, EPI_F32>(g, st); break;
         case EPI_CROSSKV: launch_t<T, EPI_CROSSKV>(g, st); break;
         case EPI_QKV_DEC: launch_t<T, EPI_QKV_DEC>(g, st); break;
-        default: fprintf(stderr, "whisper_mi355x: bad epilogue %d\n", epi); abort();
+        default: WM_FAIL("bad epilogue %d", epi);
     }
 }
 
@@ -1555,7 +1552,7 @@ static void launch_mx_t(int epi, const GemmArgs& g, const float* sa, const float
             if (sa) gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb);
             else gemm8p_mx_kernel<T, EPI_RESID, true><<<grid, 512, 0, st>>>(g, tn, sa, sb);
             break;
-        default: fprintf(stderr, "whisper_mi355x: fp8 GEMM epilogue %d not supported\n", epi); abort();
+        default: WM_FAIL("fp8 GEMM epilogue %d not supported", epi);
     }
 }
 
@@ -1564,17 +1561,14 @@ void launch_gemm_fp8(DType dt, int epi, const GemmArgs& g, const float* a_scale,
     const bool mx_in = !a_scale && g.mx_scale && epi == EPI_RESID;
     const bool mx_out = epi == EPI_GELU_MX;
     if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || (!a_scale && !mx_in) || !b_scale ||
-        (mx_out && (g.N % 32 != 0 || !g.mx_scale || !a_scale)) || (mx_in && (g.a_rpb != g.M || g.a_rstride != g.K))) {
-        fprintf(stderr, "whisper_mi355x: fp8 gemm shape not supported (N=%d K=%d)\n", g.N, g.K);
-        abort();
-    }
+        (mx_out && (g.N % 32 != 0 || !g.mx_scale || !a_scale)) || (mx_in && (g.a_rpb != g.M || g.a_rstride != g.K))) WM_FAIL("fp8 gemm shape not supported (N=%d K=%d)", g.N, g.K);
     if (dt == DType::F16) launch_mx_t<half_t>(epi, g, a_scale, b_scale, st);
     else launch_mx_t<bf16_t>(epi, g, a_scale, b_scale, st);
 }
 
 void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, float* s, hipStream_t st) {
     if (rows <= 0) return;
-    if (K % 8 != 0) { fprintf(stderr, "whisper_mi355x: fp8 quantization needs K %% 8 == 0\n"); abort(); }
+    if (K % 8 != 0) WM_FAIL("fp8 quantization needs K %% 8 == 0");
     const unsigned grid = (unsigned)((rows + 3) / 4);
     if (dt == DType::F16) quant_rows_fp8_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)x, rows, K, (uint8_t*)q, s);
     else quant_rows_fp8_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)x, rows, K, (uint8_t*)q, s);
@@ -1582,10 +1576,7 @@ void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, f
 
 void launch_gemm(DType dt, int epi, const GemmArgs& g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0) return;
-    if (g.K % 8 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0) {
-        fprintf(stderr, "whisper_mi355x: gemm shape not supported (K=%d)\n", g.K);
-        abort();
-    }
+    if (g.K % 8 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0) WM_FAIL("gemm shape not supported (K=%d)", g.K);
     if (dt == DType::F16) launch_dt<half_t>(epi, g, st);
     else launch_dt<bf16_t>(epi, g, st);
 }

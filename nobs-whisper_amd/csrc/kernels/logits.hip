@@ -86,9 +86,11 @@ __device__ void block_argmax(float& v, int& idx, float* shv, int* shi) {
         if (shv[i] > v || (shv[i] == v && shi[i] < idx)) { v = shv[i]; idx = shi[i]; }
 }
 
-// Per-element exponentials use the hardware exp2 (__expf, a few ulp): the GPU's logits already differ
-// from the CPU's by ~1e-3, so libm-accurate exp buys no parity, and its ~20-instruction expansion per
-// element made the kernel VALU-bound.
+// Per-element exponentials over the whole row use the hardware exp2 (__expf, a few ulp): the GPU's
+// logits already differ from the CPU's by ~1e-3, so libm-accurate exp buys no parity there, and its
+// ~20-instruction expansion per element made the kernel VALU-bound. The timestamp sum (<= 1501
+// elements) uses expf: "sum p(timestamps) > max p(text)" is a threshold decision on that sum alone
+// (the log-sum-exp of the row cancels out of it).
 // The row is loaded once into registers (NPT values per thread, all loads issued back to back) and
 // every pass works on registers: a row re-read per pass from L2 with one load in flight per wave
 // made the kernel latency-bound (128 us per step at 128 rows). Per-thread accumulation runs over
@@ -185,7 +187,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
         const int i = tid + k * LT;
         if (i < v.beg) continue;
         const float lp = x.get(k) > -INFINITY ? x.get(k) - lse : -INFINITY;
-        if (lp > -INFINITY) sts += __expf(lp - mts);
+        if (lp > -INFINITY) sts += expf(lp - mts);  // libm-accurate: this sum decides the timestamp rule
     }
     sts = block_sum(sts, shf);
     const float ts_logprob = sts > 0.0f ? logf(sts) + mts : -INFINITY;
@@ -236,7 +238,7 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v, TokOut* out, float* probs,
                    hipStream_t st) {
     if (n_seq <= 0) return;
-    if (v.n_vocab > NPT * LT) { fprintf(stderr, "whisper_mi355x: vocabulary %d > %d\n", v.n_vocab, NPT * LT); abort(); }
+    if (v.n_vocab > NPT * LT) WM_FAIL("vocabulary %d > %d", v.n_vocab, NPT * LT);
     logits_kernel<<<n_seq, LT, (size_t)NPT_LDS * LT * sizeof(float), st>>>(logits, ld, ctl, v, out, probs);
 }
 

@@ -177,8 +177,7 @@ void launch_layernorm_fp8(const float* x, int M, int D, const float* w, const fl
     }
     WM_LN8(6) WM_LN8(8) WM_LN8(12) WM_LN8(16) WM_LN8(20) WM_LN8(24) WM_LN8(32)
 #undef WM_LN8
-    fprintf(stderr, "whisper_mi355x: layernorm width %d > 2048\n", D);
-    abort();
+    WM_FAIL("layernorm width %d > 2048", D);
 }
 
 // TE: the token-embedding table's type: the MFMA type, or f32 for a quantized GGML embedding that
@@ -216,7 +215,7 @@ __global__ void __launch_bounds__(256) embed_ln_kernel(const TE* __restrict__ te
 void launch_embed_ln(DType dt, const void* te, bool te_f32, const float* pe, const int* tok, const int* pos, int n, int D,
                      float* x, const float* w, const float* b, void* y, hipStream_t st) {
     if (n <= 0) return;
-    if (D > 2048) { fprintf(stderr, "whisper_mi355x: embed LN width %d > 2048\n", D); abort(); }
+    if (D > 2048) WM_FAIL("embed LN width %d > 2048", D);
 #define WM_ELN(T, NPT)                                                                                                    \
     if (te_f32) embed_ln_kernel<T, NPT, float><<<n, 256, 0, st>>>((const float*)te, pe, tok, pos, D, x, w, b, (T*)y);       \
     else embed_ln_kernel<T, NPT, T><<<n, 256, 0, st>>>((const T*)te, pe, tok, pos, D, x, w, b, (T*)y)
@@ -240,8 +239,7 @@ void launch_layernorm(DType dt, const float* x, const int* rows, int M, int D, c
     }
     WM_LN(1) WM_LN(2) WM_LN(4) WM_LN(6) WM_LN(8) WM_LN(12) WM_LN(16) WM_LN(20) WM_LN(24) WM_LN(32)
 #undef WM_LN
-    fprintf(stderr, "whisper_mi355x: layernorm width %d > 2048\n", D);
-    abort();
+    WM_FAIL("layernorm width %d > 2048", D);
 }
 
 void launch_embed(DType dt, const void* te, bool te_f32, const float* pe, const int* tok, const int* pos, int n, int D,

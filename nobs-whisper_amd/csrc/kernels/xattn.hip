@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
 template <typename T, int NW, int CT, int AUX>
 __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
                                                              const T* __restrict__ qx, int Tn, int splits, float thr,
-                                                             float* __restrict__ opart, float* __restrict__ ml) {
+                                                             float* __restrict__ opart, float* __restrict__ ml, int rev) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
@@ -201,8 +201,11 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         prow[k] = row;
         poff[k] = xphys(row, pc) * 8;
     }
+    // rev: the split's tiles in reverse order (odd decoder layers: the tiles a workgroup read last in
+    // the previous layer, the most recently used lines of the die-level cache, come first)
+    auto tile_of = [&](int t) { return tb + (rev ? ntile - 1 - t : t); };
     auto issue = [&](int t) {
-        const int row0 = (tb + t) * 16;
+        const int row0 = tile_of(t) * 16;
         u32x4* st = stg + (t % NS) * TILE;
 #pragma unroll
         for (int k = 0; k < CT; k++) {
@@ -278,7 +281,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             for (int w = 0; w < NW; w++) {
                 sv += red[(w * 16 + r) * RSR + h];
             }
-            const float s2 = (tb + t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
+            const float s2 = tile_of(t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
             const float mx = max16(s2);
             float alpha = 1.0f;
             if (mx > m_run + thr) {  // first tile (m_run = -inf) or the max moved by more than thr
@@ -497,7 +500,7 @@ void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, 
 
 template <typename T>
 static void launch_step_t(const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits, float thr,
-                          float* opart, float* ml, hipStream_t st) {
+                          float* opart, float* ml, int rev, hipStream_t st) {
     dim3 grid(splits, n);
     // E is streamed once per launch (491 MB at batch 128: more than the MALL holds), so its LDS-DMA
     // loads are non-temporal (aux = 2): 86.6 vs 102.4 us per decode launch, 3075 vs 2921 audio-s/s.
@@ -505,35 +508,32 @@ static void launch_step_t(const void* enc, const int* slot, const void* qx, int 
     static const int aux = getenv("WHISPER_MI355X_XNT") ? atoi(getenv("WHISPER_MI355X_XNT")) : 2;
 #define WM_XSTEP(NW_, CT_)                                                                                                \
     if (aux == 2)                                                                                                          \
-        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml); \
+        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev); \
     else                                                                                                                   \
-        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml)
+        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev)
     switch (d) {
         case 384: WM_XSTEP(4, 3); break;
         case 512: WM_XSTEP(8, 2); break;
         case 768: WM_XSTEP(8, 3); break;
         case 1024: WM_XSTEP(8, 4); break;
         case 1280: WM_XSTEP(8, 5); break;
-        default: fprintf(stderr, "whisper_mi355x: direct cross attention needs d in {384,512,768,1024,1280}\n"); abort();
+        default: WM_FAIL("direct cross attention needs d in {384,512,768,1024,1280}");
     }
 #undef WM_XSTEP
 }
 
 void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
-                       float thr, float* opart, float* ml, hipStream_t st) {
+                       float thr, float* opart, float* ml, hipStream_t st, int rev) {
     if (n <= 0) return;
-    if (splits < 1 || splits > 16 || splits > (Tn + 15) / 16) {
-        fprintf(stderr, "whisper_mi355x: bad split count %d\n", splits);
-        abort();
-    }
-    if (dt == DType::F16) launch_step_t<half_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
-    else launch_step_t<bf16_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
+    if (splits < 1 || splits > 16 || splits > (Tn + 15) / 16) WM_FAIL("bad split count %d", splits);
+    if (dt == DType::F16) launch_step_t<half_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, rev, st);
+    else launch_step_t<bf16_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, rev, st);
 }
 
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st) {
     if (n <= 0) return;
-    if (splits > 16 || d % 128 || d > 1280) { fprintf(stderr, "whisper_mi355x: combine shape not supported\n"); abort(); }
+    if (splits > 16 || d % 128 || d > 1280) WM_FAIL("combine shape not supported");
     dim3 grid(H, cdiv(n, 16));
     if (dt == DType::F16)
         xattn_combine_kernel<half_t><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);

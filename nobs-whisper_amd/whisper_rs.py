@@ -157,6 +157,7 @@ def lib() -> C.CDLL:
         "whisper_mi355x_get_mel": (C.c_int, [vp, fp, C.c_int]),
         "whisper_mi355x_get_encoder_out": (C.c_int, [vp, fp, C.c_int]),
         "whisper_mi355x_state_stream": (vp, [vp]),
+        "whisper_mi355x_state_info": (C.c_int, [vp, ip]),
         "whisper_mi355x_weight_arena": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
         "whisper_mi355x_rccl_unique_id": (C.c_int, [C.c_char_p]),
         "whisper_mi355x_broadcast_weights": (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int]),
@@ -318,10 +319,22 @@ class WhisperState:
 
     def decisions(self, job: int = 0) -> list:
         """Per-window temperature-fallback decisions of the last full (job 0) / full_batch call."""
-        buf = (WindowDecision * 256)()
-        n = self.L.whisper_mi355x_window_decisions(self.ptr, job, buf, 256)
+        cap = 256
+        buf = (WindowDecision * cap)()
+        n = self.L.whisper_mi355x_window_decisions(self.ptr, job, buf, cap)
+        if n < 0:  # more windows than the buffer holds (> ~2 h of audio): retry with the returned count
+            cap = -n
+            buf = (WindowDecision * cap)()
+            n = self.L.whisper_mi355x_window_decisions(self.ptr, job, buf, cap)
         assert n >= 0, n
         return [{f: getattr(d, f) for f, _ in WindowDecision._fields_ if f != "pad"} for d in buf[:n]]
+
+    def info(self) -> dict:
+        """whisper_mi355x_state_info: cross form of the last call, workspace slots, cross-cache slots,
+        decode graphs kept, whether the state came from the context's pool."""
+        out = (C.c_int * 5)()
+        assert self.L.whisper_mi355x_state_info(self.ptr, out) == 5
+        return dict(direct=bool(out[0]), cap_jobs=out[1], cap_cross=out[2], graphs=out[3], pooled=bool(out[4]))
 
     def phase_ms(self):
         out = (C.c_double * 5)()

@@ -431,6 +431,9 @@ struct State {
     float no_speech_prob = 0.0f;
     // diagnostics for tests: per greedy step the top-2 log-probability gap of the chosen token
     std::vector<float> step_margin;
+    std::vector<int> step_token, step_seek;  // the greedy choice of each such step and its window's seek
+    std::vector<int> seg_seek;               // per result segment: the seek of the window it came from
+    int cur_seek = 0;
     // per decoded window: the temperature-fallback decisions (the record whisper_mi355x.h exposes)
     struct Decision { int seek, temp_idx, failed0, logprob_fail0, result_len0, no_speech; float avg_logprob0, entropy0, no_speech_prob, pad; };
     std::vector<Decision> decisions;
@@ -669,6 +672,8 @@ static TokenData sample_token(Model& m, State& s, Decoder& dec, bool best) {
         // how far the greedy choice is from flipping: its top-2 log-probability gap, or the gap of the
         // timestamp rule (timestamp mass vs best text token) that shaped this step's candidates
         s.step_margin.push_back(std::min(second > 0.0f ? logf(r.p) - logf(second) : 1e9f, dec.ts_gap));
+        s.step_token.push_back(r.id);
+        s.step_seek.push_back(s.cur_seek);
     } else {
         std::discrete_distribution<> dist(probs.begin(), probs.end());
         r.id = dist(dec.rng);
@@ -716,7 +721,10 @@ static int lang_auto_detect(Model& m, State& s) {
 // [ext] whisper_full_with_state, greedy strategy (whisper-rs Greedy{best_of:1}, whisper.rs:88)
 static int full(Model& m, State& s, OracleParams p, const float* samples, int n_samples) {
     s.result.clear();
+    s.seg_seek.clear();
     s.step_margin.clear();
+    s.step_token.clear();
+    s.step_seek.clear();
     s.decisions.clear();
     if (n_samples > 0) s.n_len = mel_compute(samples, n_samples, m.filters.data(), m.filt_n_mel, m.filt_n_fft, s.mel, &s.n_len_org, m.n_threads);
     const Vocab& vocab = m.vocab;
@@ -766,6 +774,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
         if (seek + delta_min >= seek_end) break;
         encode(m, s.mel, s.n_len, seek, s.enc);
         compute_cross(m, s);
+        s.cur_seek = seek;
         if (seek > seek_start && seek + 500 >= seek_end) prompt_past.clear();
         State::Decision dn{};
         dn.seek = seek;
@@ -880,6 +889,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
                     for (int j = i0; j < (int)toks.size(); j++) s.result.back().tokens.push_back(toks[j]);
                 }
             }
+            s.seg_seek.resize(s.result.size(), seek);
             seek += seek_delta;
         }
     }
@@ -984,6 +994,13 @@ void oracle_decisions(void* sp, void* out) {
     memcpy(out, d.data(), d.size() * sizeof(State::Decision));
 }
 int oracle_n_steps(void* sp) { return (int)((State*)sp)->step_margin.size(); }
+// per greedy step (all windows, in decode order): the chosen token and the seek of its window
+void oracle_step_tokens(void* sp, int* tok, int* seek) {
+    const State& s = *(State*)sp;
+    std::copy(s.step_token.begin(), s.step_token.end(), tok);
+    std::copy(s.step_seek.begin(), s.step_seek.end(), seek);
+}
+int oracle_segment_seek(void* sp, int i) { return ((State*)sp)->seg_seek.at(i); }
 void oracle_step_margins(void* sp, float* out) { auto& v = ((State*)sp)->step_margin; std::copy(v.begin(), v.end(), out); }
 // last decoder attempt's full token list (ids) before result_len truncation is not kept; expose the final
 int oracle_decoder_tokens(void* sp, int* out, int cap) {

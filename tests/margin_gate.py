@@ -1,0 +1,55 @@
+"""The close-call margin gate for reduced-precision runs (bf16, fp8) against the f16-numerics oracle.
+
+A greedy decode of lower precision may flip a choice the oracle made by a small margin, never a
+confident one. For every token the oracle kept in its segments this module gives the smallest
+margin (top-2 log-probability gap, or the gap of the "sum p(timestamps) > max p(text)" rule) over
+the oracle's decode steps since the previous kept token of the same window, up to and including
+its own; a flip on a dropped step (a segment-opening timestamp) surfaces at the next kept token.
+
+Multi-window runs (> 30 s, or a window that ends early): the oracle records the window (seek) of
+every step and of every segment, so each window's kept tokens are aligned with that window's own
+steps. Comparison stops at the first difference: later windows depend on the earlier ones' seek
+and prompt carry-over. Use with temperature_inc = 0 (one greedy attempt per window).
+"""
+
+
+def kept_token_margins(ref):
+    """(tokens, margins) of the oracle result `ref` (oracle_py.Oracle.full), flattened over windows."""
+    seeks = ref["step_seeks"]
+    toks = ref["step_tokens"]
+    marg = [float(x) for x in ref["margins"]]
+    assert len(seeks) == len(toks) == len(marg), (len(seeks), len(toks), len(marg))
+    by_seek = {}
+    for i, s in enumerate(seeks):
+        by_seek.setdefault(s, []).append(i)
+    out_t, out_m = [], []
+    pos = {}
+    for seg in ref["segments"]:
+        steps = by_seek[seg["seek"]]
+        i = pos.get(seg["seek"], 0)
+        for t in seg["tokens"]:
+            j = i
+            while toks[steps[j]] != t:
+                j += 1
+            out_t.append(t)
+            out_m.append(min(marg[steps[k]] for k in range(i, j + 1)))
+            i = j + 1
+        pos[seg["seek"]] = i
+    return out_t, out_m
+
+
+def assert_diverges_only_at_close_calls(got, exp, margins, gap, min_prefix=0):
+    """got == exp up to the first difference, which must fall on a token the oracle decided by at
+    most `gap` nats; and the identical prefix is at least min(min_prefix, len(exp)) tokens long (a
+    case whose very first steps are close calls proves nothing). Returns the prefix length."""
+    n = 0
+    while n < len(exp) and n < len(got) and got[n] == exp[n]:
+        n += 1
+    if n < len(exp) and n < len(got):
+        assert n < len(margins) and margins[n] <= gap, \
+            f"diverged at token {n} where the oracle's margin is {margins[n]:.3f} nats (> {gap})"
+    elif n < len(exp):
+        # the run ended (EOT, window end) where the oracle went on with token n: a flip of that step
+        assert margins[n] <= gap, f"ended at token {n} where the oracle's margin is {margins[n]:.3f} nats (> {gap})"
+    assert n >= min(min_prefix, len(exp)), f"identical prefix {n} < {min(min_prefix, len(exp))} tokens"
+    return n

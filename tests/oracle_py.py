@@ -99,6 +99,8 @@ def lib():
             "oracle_n_decisions": (C.c_int, [vp]),
             "oracle_decisions": (None, [vp, vp]),
             "oracle_step_margins": (None, [vp, fp]),
+            "oracle_step_tokens": (None, [vp, ip, ip]),
+            "oracle_segment_seek": (C.c_int, [vp, C.c_int]),
             "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
             "oracle_mel_tables": (None, [fp, fp, fp]),
             "oracle_tensor": (C.c_long, [vp, C.c_char_p, C.c_int, fp, C.c_long]),
@@ -218,10 +220,14 @@ class Oracle:
             t0, t1 = C.c_int64(), C.c_int64()
             self.L.oracle_segment_t(self.s, i, C.byref(t0), C.byref(t1))
             toks = [self.L.oracle_segment_token(self.s, i, j) for j in range(self.L.oracle_segment_n_tokens(self.s, i))]
-            segs.append(dict(t0=t0.value, t1=t1.value, text=self.L.oracle_segment_text(self.s, i), tokens=toks))
+            segs.append(dict(t0=t0.value, t1=t1.value, text=self.L.oracle_segment_text(self.s, i), tokens=toks,
+                             seek=self.L.oracle_segment_seek(self.s, i)))
         n = self.L.oracle_n_steps(self.s)
         margins = np.empty(n, np.float32)
         self.L.oracle_step_margins(self.s, _fp(margins))
+        step_tok = np.empty(max(1, n), np.int32)
+        step_seek = np.empty(max(1, n), np.int32)
+        self.L.oracle_step_tokens(self.s, _ip(step_tok), _ip(step_seek))
         seq = (C.c_int * 4096)()
         n_seq = min(4096, self.L.oracle_decoder_tokens(self.s, seq, 4096))
         nd = self.L.oracle_n_decisions(self.s)
@@ -229,6 +235,7 @@ class Oracle:
         self.L.oracle_decisions(self.s, C.cast(dec, C.c_void_p))
         return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
                     no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins, seq=list(seq[:n_seq]),
+                    step_tokens=step_tok[:n].tolist(), step_seeks=step_seek[:n].tolist(),
                     decisions=decisions_to_dicts(dec[:nd]))
 
 

@@ -1,10 +1,30 @@
 #!/bin/bash
-# bench A/B of two environment settings on one box: AB_A="X=1" AB_B="Y=2" [BARGS=...]
+# Same-box A/B of engine env switches on the headline bench (short runs, no extras). Usage:
+#   AB="XSERP=0 XSERP=1 XSERP=1,XNT=0" bash tools/gpu_envab.sh     (each token: comma-separated
+#   WHISPER_MI355X_<NAME>=<value> pairs; "base" = no override). Output: gpurun_out/envab_<i>.json
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-cd "$R" && mkdir -p gpurun_out
-for v in A B A B; do
-  eval envs=\$AB_$v
-  timeout -k 10 400 env BENCH_KTIME=0 $envs python bench.py --steps 2 --warmup 1 --variants 0 --frontend 0 --cpu-baseline 0 ${BARGS} > gpurun_out/eab_$v.log 2> gpurun_out/eab_$v.err
-  rc=$?; [ $rc -eq 0 ] || { echo "bench $v rc=$rc"; tail -5 gpurun_out/eab_$v.err; exit $rc; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/eab_$v.log').read().strip().splitlines()[-1]); print('$v', '$envs', d['value'], d['extra']['phase_ms_last_step'])"
+cd "$R" || exit 1
+mkdir -p gpurun_out
+ARGS="${BENCH_ARGS:---steps 4 --warmup 1 --variants 0 --cpu-baseline 0 --frontend 0 --app-pattern 0}"
+i=0
+for spec in ${AB:-base}; do
+  envs=()
+  if [ "$spec" != base ]; then
+    IFS=',' read -ra kv <<< "$spec"
+    for x in "${kv[@]}"; do envs+=("WHISPER_MI355X_$x"); done
+  fi
+  timeout -k 10 ${T_AB:-300} env "${envs[@]}" python -u bench.py $ARGS > gpurun_out/envab_$i.json 2> gpurun_out/envab_$i.err
+  rc=$?
+  python3 - "$spec" gpurun_out/envab_$i.json <<'PY'
+import json, sys
+try:
+    d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+    r = d["roofline"]
+    print(f"{sys.argv[1]:28s} value {d['value']:8.1f}  ms/step {d['ms_per_step']:8.1f}  phases {d['extra']['phase_ms_last_step']}  "
+          f"{r['kernel']} {r['avg_launch_ms']*1e3:.1f} us frac {r['frac']}")
+except Exception as e:
+    print(sys.argv[1], "no result", e)
+PY
+  [ $rc -eq 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/envab_$i.err; exit $rc; }
+  i=$((i+1))
 done
