@@ -361,6 +361,9 @@ def main():
     ap.add_argument("--variants", type=int, default=1,
                     help="also time the reference's prompted (default vocabulary) and auto-language workloads")
     ap.add_argument("--variant-steps", type=int, default=3)
+    ap.add_argument("--fallback-line", type=int, default=0,
+                    help="also time the reference's verbatim FullParams with temperature fallback (slow on "
+                         "untrained weights: most windows fall back to sampled re-decodes)")
     ap.add_argument("--frontend", type=int, default=1,
                     help="also time the GPU audio front-end (audio.rs VAD chunking + 48 kHz -> 16 kHz resampler)")
     ap.add_argument("--app-pattern", type=int, default=1,
@@ -507,20 +510,26 @@ def main():
                                  ms_per_step=round(1e3 * el / args.variant_steps, 2),
                                  prompt_tokens=len(ctx.tokenize(wrs.DEFAULT_VOCABULARY)) if "vocabulary" in name else 0,
                                  phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
-        # SURVEY.md §8d's second mode: real greedy termination (EOT and timestamps end each window, the
-        # reference's temperature fallback on: whisper.rs:88-124 verbatim), same chunks, same weights
-        p = wrs.reference_full_params("en")
-        step(p, 0)
-        el = timed(p, args.variant_steps, 0)
-        dec_tok = L.whisper_mi355x_batch_decoded_tokens(st.ptr)
-        fell_back = sum(1 for j in range(nb) for d in st.decisions(j) if d["temp_idx"] > 0)
-        variants.append(dict(workload="real greedy termination (EOT / timestamps end each window; fallback on; "
-                                      "language en, no prompt)",
-                             value=round(30.0 * global_batch * args.variant_steps / el, 2),
-                             ms_per_step=round(1e3 * el / args.variant_steps, 2),
-                             decoded_tokens_per_chunk=round(dec_tok / max(1, nb), 1),
-                             windows_fallen_back=fell_back,
-                             phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
+        # SURVEY.md §8d's second mode: real greedy termination (EOT and timestamps end each window),
+        # same chunks, same weights. temperature_inc = 0: the greedy attempt's result stands whatever
+        # its entropy / logprob (synthetic weights are not trained, so the reference's fallback would
+        # re-decode most windows with sampling: --fallback-line 1 adds that verbatim-params line)
+        lines = [("real greedy termination (EOT / timestamps end each window; greedy attempt only; "
+                  "language en, no prompt)", 0.0)]
+        if args.fallback_line:
+            lines.append(("whisper.rs:88-124 verbatim (greedy + temperature fallback; language en, no prompt)", 0.2))
+        for name, t_inc in lines:
+            p = wrs.reference_full_params("en")
+            p.temperature_inc = t_inc
+            step(p, 0)
+            el = timed(p, args.variant_steps, 0)
+            dec_tok = L.whisper_mi355x_batch_decoded_tokens(st.ptr)
+            fell_back = sum(1 for j in range(nb) for d in st.decisions(j) if d["temp_idx"] > 0)
+            variants.append(dict(workload=name, value=round(30.0 * global_batch * args.variant_steps / el, 2),
+                                 ms_per_step=round(1e3 * el / args.variant_steps, 2),
+                                 decoded_tokens_per_chunk=round(dec_tok / max(1, nb), 1),
+                                 windows=sum(len(st.decisions(j)) for j in range(nb)), windows_fallen_back=fell_back,
+                                 phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
 
     frontend = None
     if args.frontend and rank == 0 and nb:

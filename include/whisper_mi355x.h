@@ -106,6 +106,13 @@ WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cl
 WHISPER_API int whisper_mi355x_debug_gemm(struct whisper_context * ctx, int epi, const void * A, int M, int K,
                                           const void * B, int N, const float * bias, void * out, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_gemm_variant(int variant);
+/* Debug/tuning: the small-M decode GEMM (M <= 32, K % 256 == 0): out = A.B^T + bias with epilogue epi
+ * (2 residual: out f32 += ..., 4 f32, 0 store, 1 gelu); with ln_w != NULL, A is f32 [M][K] and the
+ * product uses LN(A) * ln_w + ln_b (K <= 1280). The first launch's result stays in out; reps more
+ * launches are timed (note: epi 2 accumulates into out on every launch). */
+WHISPER_API int whisper_mi355x_debug_gemm_small(struct whisper_context * ctx, int epi, const void * A, int M, int K,
+                                                const void * B, int N, const float * bias, void * out,
+                                                const float * ln_w, const float * ln_b, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
 /* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
  * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */

@@ -569,6 +569,37 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
         return 0;
     });
 }
+int whisper_mi355x_debug_gemm_small(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B,
+                                    int N, const float* bias, void* out, const float* ln_w, const float* ln_b, int reps,
+                                    float* ms) {
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || !gemm_small_ok(M, K, ln_w != nullptr)) return -1;
+        hipSetDevice(ctx->c.device);
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        GemmArgs g{};
+        g.A = A; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
+        g.B = B; g.bias = bias; g.M = M; g.N = N; g.K = K;
+        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
+        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
+        g.a_ln_w = ln_w; g.a_ln_b = ln_b;
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        launch_gemm_small(ctx->c.dt, epi, g, ln_w != nullptr, st);
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) launch_gemm_small(ctx->c.dt, epi, g, ln_w != nullptr, st);
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        return 0;
+    });
+}
 int whisper_mi355x_debug_gemm_fp8(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale, int M,
                                   int K, const void* B8, const float* b_scale, int N, const float* bias, void* out,
                                   int reps, float* ms) {

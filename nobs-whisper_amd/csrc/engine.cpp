@@ -725,6 +725,104 @@ struct DecView {
     float *xo, *xml;
 };
 
+// WHISPER_MI355X_SMALLM=0 turns the small-M decode path off (A/B): decode steps of <= 32 clips then
+// take the split-K path like larger batches
+static bool small_m_steps() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_SMALLM");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+// Decode step over <= 32 rows (the app's one clip per call, whisper.rs:83-85 / state.rs:147; one
+// rank's 16-clip shard of configs[3] at 8 GPUs), kernels only: every projection is ONE launch of
+// gemm_small_kernel (no split-K slabs, no reduce launch), and the LayerNorm in front of the QKV,
+// cross-Q and FC1 projections runs in that GEMM's prologue from the f32 residual stream. Per layer:
+// QKV (raw f32 sums) -> self attention (bias, scale, cache append, attention) -> Wo (+x) -> cross-Q
+// -> cross attention -> Wxo (+x) -> FC1 (GELU) -> FC2 (+x): 8 launches in the cache form, against
+// 15 on the split-K path. Results per row do not depend on the other rows (batch == single within
+// this path); they differ in the last bits from the split-K path's (another summation order).
+static void decoder_rows_small(Context* c, whisper_state* s, const DecView& v, bool xdirect, double self_share,
+                               int kt_stride) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_text_state, H = hp.n_text_head, V = hp.n_vocab, L = hp.n_text_layer;
+    const DType dt = c->dt;
+    const Weights& W = c->w;
+    const size_t E = esize(dt);
+    hipStream_t st = v.st;
+    const int n = v.n;
+    int* tok = w.tok + v.r0;
+    int* pos = w.pos + v.r0;
+    int* slot = w.slot + v.r0;
+    int* nkv_cross = w.nkv_cross + v.r0;
+    float* dx = w.dx + (size_t)v.r0 * d;
+    void* dh = (char*)w.dh + (size_t)v.r0 * d * E;
+    void* dq = (char*)w.dq + (size_t)v.r0 * d * E;
+    void* datt = (char*)w.datt + (size_t)v.r0 * d * E;
+    void* dff = (char*)w.dff + (size_t)v.r0 * 4 * d * E;
+    void* qx = w.qx ? (void*)((char*)w.qx + (size_t)v.r0 * 2 * H * d * E) : nullptr;
+    float* raw = v.splitk;  // f32 projection sums handed to the attention prologues ([n][3d] / [n][d])
+    const double kvrow = (double)H * 64 * 2 * 2;
+    auto small = [&](int epi, const void* A, int K, const void* Wt, int N, const float* bias, void* out, long ldo,
+                     const float* lnw = nullptr, const float* lnb = nullptr) {
+        GemmArgs g = gemm_plain(A, n, K, Wt, N, bias, out, ldo);
+        g.a_ln_w = lnw;
+        g.a_ln_b = lnb;
+        KT kt(s, K_GEMM_DEC, 2.0 * N * K + 2.0 * n * K + 4.0 * n * N, st);
+        launch_gemm_small(dt, epi, g, lnw != nullptr, st);
+    };
+    launch_embed(dt, W.tok_emb_f32 ? (const void*)W.tok_emb_f32 : W.tok_emb, W.tok_emb_f32 != nullptr, W.pos_d, tok, pos, n, d,
+                 dx, st);
+    for (int l = 0; l < L; l++) {
+        const LayerW& Lw = W.dec[l];
+        const bool kt_layer = l % kt_stride == 0;
+        // self attention: LN1 in the QKV GEMM, raw sums to the attention prologue (+ bias, q/k scale)
+        small(EPI_F32, dx, d, Lw.wqkv, 3 * d, nullptr, raw, 3 * d, Lw.ln1_w, Lw.ln1_b);
+        {
+            const DecSlabs sl{raw, 1, (long)n * 3 * d, 3 * d, Lw.bqkv, c->k_scale};
+            KT kt(s, K_ATTN_SELF, self_share, st, kt_layer);
+            launch_attn_self_step(dt, sl, w.self, slot, pos, n, L, l, H, hp.n_text_ctx, d, datt, st);
+        }
+        small(EPI_RESID, datt, d, Lw.wo, d, Lw.bo, dx, d);
+        if (xdirect) {
+            GemmArgs g = gemm_plain(dx, n, d, Lw.wxq, d, Lw.bxq, dq, d);
+            g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
+            g.a_ln_w = Lw.lnx_w; g.a_ln_b = Lw.lnx_b;
+            {
+                KT kt(s, K_GEMM_DEC, 2.0 * d * d + 2.0 * n * d + 4.0 * n * d, st);
+                launch_gemm_small(dt, EPI_STORE, g, true, st);
+            }
+            const int Ta = hp.n_audio_ctx, S = xattn_splits(n, Ta);
+            {
+                KT kt(s, K_GEMM_DEC, 2.0 * d * d + 2.0 * n * d + 4.0 * n * H * d, st);
+                launch_xattn_qproj(dt, dq, (const char*)W.wkT + (size_t)l * H * d * 64 * 2, n, d, H, c->k_scale, qx, st);
+            }
+            {
+                KT kt(s, K_ATTN_CROSS, (double)n * Ta * d * 2, st, kt_layer);
+                launch_xattn_step(dt, w.enc, slot, qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st, xattn_serp() ? (l & 1) : 0);
+            }
+            {
+                KT kt(s, K_GEMM_DEC, 2.0 * d * d + 4.0 * n * S * d + 2.0 * n * d, st);
+                launch_xattn_combine(dt, v.xo, v.xml, S, (const char*)W.wkv_cross + (size_t)(2 * l + 1) * d * d * 2,
+                                     W.bkv_cross + (size_t)(2 * l + 1) * d, n, d, H, datt, st);
+            }
+        } else {
+            small(EPI_F32, dx, d, Lw.wxq, d, nullptr, raw, d, Lw.lnx_w, Lw.lnx_b);
+            const DecSlabs sl{raw, 1, (long)n * d, d, Lw.bxq, c->k_scale};
+            KT kt(s, K_ATTN_CROSS, (double)n * hp.n_audio_ctx * kvrow, st, kt_layer);
+            launch_attn_cross_step(dt, sl, w.cross, slot, nkv_cross, n, L, l, H, hp.n_audio_ctx, d, datt, st);
+        }
+        small(EPI_RESID, datt, d, Lw.wxo, d, Lw.bxo, dx, d);
+        small(EPI_GELU, dx, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d, Lw.ln2_w, Lw.ln2_b);
+        small(EPI_RESID, dff, 4 * d, Lw.w2, d, Lw.b2, dx, d);
+    }
+    launch_layernorm(dt, dx, nullptr, n, d, W.lnd_w, W.lnd_b, dh, st);
+    GemmArgs g = gemm_plain(dh, n, d, W.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
+    tgemm_ws(s, K_GEMM_DEC, dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
+}
+
 // The decoder forward over the view's tokens + logits; kernels only (graph-capturable). `fused`
 // (decode steps: one token per clip, logits for every row, <= 128 rows per view): every LayerNorm
 // is folded into the embedding or into the split-K reduce of the preceding residual GEMM.
@@ -786,6 +884,10 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
     // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
     const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
+    if (fused && !w8 && small_m_steps() && gemm_small_ok(n_tok, d, true) && gemm_small_ok(n_tok, 4 * d, false)) {
+        decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
+        return;
+    }
     for (int l = 0; l < L; l++) {
         const LayerW& Lw = W.dec[l];
         static const Context::Fp8Dec no8{};

@@ -62,6 +62,9 @@ struct GemmArgs {
     // EPI_RESID on the split-K path only: fused LayerNorm of the updated residual rows,
     // ln_out[m][:] = LN(out[m][:]) * ln_w + ln_b (the next GEMM's input; null = no LN)
     const float* ln_w; const float* ln_b; void* ln_out;
+    // small-M decode GEMM (launch_gemm_small) with lna: A is the f32 residual stream and the
+    // workgroup applies LN(A) * a_ln_w + a_ln_b (ggml_norm) to its rows before the product
+    const float* a_ln_w; const float* a_ln_b;
     // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
     // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
     uint8_t* mx_scale;
@@ -86,6 +89,12 @@ void init_gelu_table();
 // a.splitk_ws, no epilogue; the consumer reduces them (attention prologues). Returns the split
 // count, or 0 when the shape/workspace does not allow it (the caller then uses launch_gemm).
 int launch_gemm_partials(DType dt, const GemmArgs& a, hipStream_t st);
+// Decode steps of M <= 32 rows: one launch, no split-K slabs and no reduce launch (one workgroup =
+// 16 output columns over the whole K, its 8 waves splitting K and summing in LDS). Epilogues
+// EPI_F32 / EPI_STORE / EPI_GELU / EPI_RESID. lna: A = LN(f32 residual rows) computed in the
+// prologue (K <= 1280). Returns false when the shape is not supported (K % 256, M > 32).
+bool gemm_small_ok(int M, int K, bool lna);
+void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream_t st);
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------
 // encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)

@@ -1336,6 +1336,152 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
     *(uint2*)((T*)g.ln_out + (long)m * g.N + n) = *(const uint2*)y;
 }
 
+// Decode steps of <= 32 active clips (the app's one clip per call, whisper.rs:83-85; one rank's shard
+// of configs[3] at 8 GPUs): one workgroup = 16 output columns x all M rows x the whole K. Its 8 waves
+// split K (wave w: k in [w*K/8, (w+1)*K/8)) and add their partial sums in LDS in wave order, so no
+// split-K slab leaves the chip and no reduce launch follows. Weights are read once, by 16-byte loads
+// straight into the B fragments (a chunk of K-steps in flight before its MFMAs, the next chunk issued
+// before the current one is consumed); the <= 32 activation rows are re-read from L2 by every
+// workgroup. LNA: A is the f32 residual stream; the workgroup applies ggml_norm (double sums, f32
+// mean / variance, (v*scale)*w + b separately rounded, as block256_layernorm) to its rows in the
+// prologue, into an LDS image, so the LayerNorm launch of the split-K path disappears too.
+template <typename T, int EPI, bool LNA, int NR>
+__global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
+#pragma clang fp contract(off)
+    typedef typename Frag<T>::type FT;
+    constexpr int NW = 8, CH = 5;  // waves; K-steps (32 each) per load chunk
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int n0 = blockIdx.x * 16, K = g.K;
+    const int lda = K + 8;  // LDS row stride of the LNA image (16-byte pad: conflict-free b128 reads)
+    T* aimg = (T*)smem;
+    float* red = (float*)(smem + (LNA ? (size_t)NR * 16 * lda * sizeof(T) : 0));
+    const u32x4 zero = {0, 0, 0, 0};
+    if constexpr (LNA) {
+        for (int r = wave; r < NR * 16; r += NW) {
+            T* ar = aimg + (long)r * lda;
+            if (r >= g.M) {
+                for (int c = lane * 8; c < K; c += 512) *(u32x4*)(ar + c) = zero;
+                continue;
+            }
+            const float* xr = (const float*)g.A + (long)r * g.a_rstride;
+            float v[20];  // K <= 1280: lane holds columns lane + 64j
+#pragma unroll
+            for (int j = 0; j < 20; j++) v[j] = lane + 64 * j < K ? xr[lane + 64 * j] : 0.0f;
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 20; j++) s += (double)v[j];
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            const float mean = (float)(s / K);
+            double s2 = 0.0;
+#pragma unroll
+            for (int j = 0; j < 20; j++)
+                if (lane + 64 * j < K) {
+                    v[j] = v[j] - mean;
+                    s2 += (double)(v[j] * v[j]);
+                }
+            for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+            const float scale = 1.0f / sqrtf((float)(s2 / K) + 1e-5f);
+#pragma unroll
+            for (int j = 0; j < 20; j++) {
+                const int c = lane + 64 * j;
+                if (c < K) ar[c] = (T)((v[j] * scale) * g.a_ln_w[c] + g.a_ln_b[c]);
+            }
+        }
+        __syncthreads();
+    }
+    const int kw = K / NW, nst = kw / 32;
+    const int k0 = wave * kw + 8 * (lane >> 4);
+    const T* bp = (const T*)g.B + (long)min(n0 + (lane & 15), g.N - 1) * K + k0;
+    const T* ap[NR];
+    bool arow[NR];
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const int r = i * 16 + (lane & 15);
+        arow[i] = r < g.M;
+        ap[i] = LNA ? aimg + (long)r * lda + k0 : (const T*)g.A + (long)min(r, g.M - 1) * g.a_rstride + k0;
+    }
+    f32x4 acc[NR];
+#pragma unroll
+    for (int i = 0; i < NR; i++) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    u32x4 bq[2][CH], aq[2][NR][CH];
+    auto load = [&](int c, u32x4 (&b)[CH], u32x4 (&a)[NR][CH]) {
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            const int st = c * CH + u;
+            b[u] = st < nst ? __builtin_nontemporal_load((const u32x4*)(bp + 32 * st)) : zero;
+#pragma unroll
+            for (int i = 0; i < NR; i++) a[i][u] = st < nst && arow[i] ? *(const u32x4*)(ap[i] + 32 * st) : zero;
+        }
+    };
+    auto mma = [&](const u32x4 (&b)[CH], const u32x4 (&a)[NR][CH]) {
+#pragma unroll
+        for (int u = 0; u < CH; u++)
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+                acc[i] = mfma16x16x32(__builtin_bit_cast(FT, a[i][u]), __builtin_bit_cast(FT, b[u]), acc[i]);
+    };
+    const int nch = (nst + CH - 1) / CH;  // <= 4 (K <= 5120)
+    load(0, bq[0], aq[0]);
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) load(c + 1, bq[1], aq[1]);
+        mma(bq[0], aq[0]);
+        if (c + 1 < nch) {
+            if (c + 2 < nch) load(c + 2, bq[0], aq[0]);
+            mma(bq[1], aq[1]);
+        }
+    }
+    // partial sums of the 8 waves -> LDS, summed in wave order
+#pragma unroll
+    for (int i = 0; i < NR; i++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) red[((wave * NR + i) * 16 + 4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[i][r];
+    __syncthreads();
+    if (tid < NR * 256) {
+        const int i = tid >> 8, row = (tid >> 4) & 15, col = tid & 15;
+        const int m = i * 16 + row, n = n0 + col;
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NW; w++) v += red[((w * NR + i) * 16 + row) * 16 + col];
+        if (m < g.M && n < g.N) epilogue<EPI, T>(g, m, n, v);
+    }
+}
+
+bool gemm_small_ok(int M, int K, bool lna) { return M >= 1 && M <= 32 && K % 256 == 0 && K <= 5120 && (!lna || K <= 1280); }
+
+template <typename T, int EPI>
+static void launch_small_t(const GemmArgs& g, bool lna, hipStream_t st) {
+    const int nr = g.M <= 16 ? 1 : 2;
+    const size_t red = (size_t)8 * nr * 256 * sizeof(float);
+    const size_t img = lna ? (size_t)nr * 16 * (g.K + 8) * sizeof(T) : 0;
+    const unsigned grid = cdiv(g.N, 16);
+    if (lna) {
+        if (nr == 1) gemm_small_kernel<T, EPI, true, 1><<<grid, 512, img + red, st>>>(g);
+        else gemm_small_kernel<T, EPI, true, 2><<<grid, 512, img + red, st>>>(g);
+    } else {
+        if (nr == 1) gemm_small_kernel<T, EPI, false, 1><<<grid, 512, red, st>>>(g);
+        else gemm_small_kernel<T, EPI, false, 2><<<grid, 512, red, st>>>(g);
+    }
+}
+
+template <typename T>
+static void launch_small_dt(int epi, const GemmArgs& g, bool lna, hipStream_t st) {
+    switch (epi) {
+        case EPI_STORE: launch_small_t<T, EPI_STORE>(g, lna, st); break;
+        case EPI_GELU: launch_small_t<T, EPI_GELU>(g, lna, st); break;
+        case EPI_RESID: launch_small_t<T, EPI_RESID>(g, lna, st); break;
+        case EPI_F32: launch_small_t<T, EPI_F32>(g, lna, st); break;
+        default: WM_FAIL("small-M GEMM epilogue %d not supported", epi);
+    }
+}
+
+void launch_gemm_small(DType dt, int epi, const GemmArgs& g, bool lna, hipStream_t st) {
+    if (g.M <= 0 || g.N <= 0) return;
+    if (!gemm_small_ok(g.M, g.K, lna)) WM_FAIL("small-M GEMM shape not supported (M=%d K=%d)", g.M, g.K);
+    if (dt == DType::F16) launch_small_dt<half_t>(epi, g, lna, st);
+    else launch_small_dt<bf16_t>(epi, g, lna, st);
+}
+
 int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
 static int dec_splits_override() { return g_dec_splits; }
 // decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU; default), or

@@ -62,7 +62,7 @@ def test_unsupported_sample_rate_returns_error(wrs):
     """audio.rs-style silence search at a sample rate whose 20 ms window does not fit the kernel's LDS
     staging (4 MHz: 80000-sample windows): -1, not an abort; a supported rate works afterwards."""
     L = wrs.lib()
-    x = synthetic_pcm(0, seconds=2.0)
+    x = synthetic_pcm(0, seconds=10.0)  # 160000 samples: two 20 ms windows at 4 MHz
     ptrs = (C.c_void_p * 1)(x.ctypes.data)
     n = (C.c_int * 1)(len(x))
     counts = (C.c_int * 1)()

@@ -154,3 +154,48 @@ def test_gemm_gelu_epilogue(wrs, ctx, M, N, K):
     ref = _gelu_ggml(pre)
     same = (got.view(np.uint16) == ref.view(np.uint16)) | (got.astype(np.float32) == ref.astype(np.float32))
     assert same.all(), f"{(~same).sum()} of {same.size} differ, e.g. pre {pre[~same][:4]} got {got[~same][:4]} ref {ref[~same][:4]}"
+
+
+@pytest.mark.parametrize("M,N,K,epi,lna", [(1, 1280, 1280, 4, True), (16, 3840, 1280, 4, True), (32, 1280, 1280, 2, False),
+                                           (17, 1280, 5120, 2, False), (7, 5120, 1280, 4, True), (32, 384, 1536, 4, False),
+                                           (3, 1536, 512, 4, True)])
+def test_gemm_small_matches_numpy(wrs, ctx, M, N, K, epi, lna):
+    """Decode steps of <= 32 rows (gemm_small_kernel: 16 columns per workgroup over the whole K, the
+    8 waves' partial sums added in LDS; no split-K slabs): f32 output (epi 4) or the residual add (epi
+    2), and with lna the LayerNorm of the f32 input rows applied in the prologue (ggml_norm, rounded
+    to the MFMA type like the split-K path's fused reduce + LN)."""
+    L = wrs.lib()
+    L.whisper_mi355x_debug_gemm_small.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                                  C.POINTER(C.c_float)]
+    rng = np.random.default_rng(M * 11 + N + K)
+    B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    w = (1.0 + 0.1 * rng.standard_normal(K)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(K)).astype(np.float32)
+    if lna:
+        X = (3.0 * rng.standard_normal((M, K)) + 0.5).astype(np.float32)
+        mu = X.astype(np.float64).mean(1, keepdims=True)
+        var = ((X.astype(np.float64) - mu) ** 2).mean(1, keepdims=True)
+        A64 = ((X - mu) / np.sqrt(var + 1e-5) * w + b).astype(np.float16).astype(np.float64)
+        A = X
+    else:
+        A = rng.standard_normal((M, K)).astype(np.float16)
+        A64 = A.astype(np.float64)
+    x0 = rng.standard_normal((M, N)).astype(np.float32)
+    out = x0.copy() if epi == 2 else np.zeros((M, N), np.float32)
+    ptrs = [_dev(wrs, ctx, a) for a in (A, B, bias, out, w, b)]
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_gemm_small(ctx.ptr, epi, C.c_void_p(ptrs[0]), M, K, C.c_void_p(ptrs[1]), N,
+                                             C.c_void_p(ptrs[2]), C.c_void_p(ptrs[3]),
+                                             C.c_void_p(ptrs[4]) if lna else None, C.c_void_p(ptrs[5]) if lna else None,
+                                             0, C.byref(ms)) == 0
+    L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(ptrs[3]), out.nbytes, 2)
+    for p in ptrs:
+        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
+    B64 = B.astype(np.float64)
+    ref = A64 @ B64.T + bias + (x0 if epi == 2 else 0.0)
+    # lna: an operand rounded one f16 ulp differently from numpy's LN moves a product by <= 2^-10 |a b|
+    bound = (2e-3 if lna else 1e-4) * (np.abs(A64) @ np.abs(B64).T) + 1e-5 + 1e-6 * np.abs(ref)
+    err = np.abs(out - ref)
+    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"

@@ -13,9 +13,9 @@ for spec in ${AB:-base}; do
     IFS=',' read -ra kv <<< "$spec"
     for x in "${kv[@]}"; do envs+=("WHISPER_MI355X_$x"); done
   fi
-  timeout -k 10 ${T_AB:-300} env "${envs[@]}" python -u bench.py $ARGS > gpurun_out/envab_$i.json 2> gpurun_out/envab_$i.err
+  timeout -k 10 ${T_AB:-300} env "${envs[@]}" python -u bench.py $ARGS > gpurun_out/${OUTP:-envab}_$i.json 2> gpurun_out/${OUTP:-envab}_$i.err
   rc=$?
-  python3 - "$spec" gpurun_out/envab_$i.json <<'PY'
+  python3 - "$spec" gpurun_out/${OUTP:-envab}_$i.json <<'PY'
 import json, sys
 try:
     d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
@@ -25,6 +25,6 @@ try:
 except Exception as e:
     print(sys.argv[1], "no result", e)
 PY
-  [ $rc -eq 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/envab_$i.err; exit $rc; }
+  [ $rc -eq 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/${OUTP:-envab}_$i.err; exit $rc; }
   i=$((i+1))
 done

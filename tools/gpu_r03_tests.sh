@@ -26,4 +26,7 @@ fi
 if [ -n "$AB" ]; then
   bash tools/gpu_envab.sh || exit $?
 fi
+if [ -n "$AB2" ]; then
+  AB="$AB2" BENCH_ARGS="$BENCH_ARGS2" OUTP=envab2 bash tools/gpu_envab.sh || exit $?
+fi
 exit $final
