@@ -58,6 +58,10 @@ static whisper_context* make_ctx(const char* path, whisper_context_params cp, in
         delete w;
         return nullptr;
     }
+    if (w->c.quant && w->c.fp8_enc) {  // the e4m3 weights are quantized from compute-type matrices
+        fprintf(stderr, "whisper_mi355x: fp8 mode needs an f16 model file; %s is block-quantized, fp8 off\n", path);
+        w->c.fp8_enc = false;
+    }
     w->c.owner = w;
     return w;
 }

@@ -265,7 +265,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.mxs); dfree(w.qtiles);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.mxs); dfree(w.qtiles); dfree(w.wdq);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
     if (w.h_tout) hipHostFree(w.h_tout);
@@ -408,6 +408,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         dalloc(w.xml, xo_rows * H * 2 * 4);
     }
     if (!s->direct) ensure_cross(c, w, n_jobs);
+    if (c->quant && !w.wdq) dalloc(w.wdq, (size_t)16 * d * d * E);
 }
 
 static void ensure_ws(Context* c, whisper_state* s, int n_jobs) {
@@ -574,6 +575,32 @@ static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float*
     launch_gemm_fp8(s->ctx->dt, epi, g, sa, sb, st);
 }
 
+// Projection weights of one layer in the compute type: the arena's matrices, or, for a block-quantized
+// file, the layer's blocks dequantized into the state's scratch (one layer at a time, on the stream
+// that then runs the layer: the encoder and the prefill are big-M GEMMs that read every weight many
+// times, so they read a dequantized copy; decode steps read the blocks themselves, gemm_small_kernel)
+struct LayerMats { const void *wqkv, *wo, *wxq, *wxo, *w1, *w2; };
+static LayerMats layer_mats(Context* c, whisper_state* s, const LayerW& L, hipStream_t st) {
+    LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
+    if (!c->quant) return m;
+    const int d = c->hp.n_audio_state;
+    const size_t E = esize(c->dt);
+    char* p = (char*)s->ws.wdq;
+    auto one = [&](const QMat& q, long rows, int K, const void*& dst) {
+        if (!q.type) return;
+        launch_dequant(c->dt, q, rows, K, p, st);
+        dst = p;
+        p += (size_t)rows * K * E;
+    };
+    one(L.qqkv, 3L * d, d, m.wqkv);
+    one(L.qo, d, d, m.wo);
+    one(L.qxq, d, d, m.wxq);
+    one(L.qxo, d, d, m.wxo);
+    one(L.q1, 4L * d, d, m.w1);
+    one(L.q2, d, 4 * d, m.w2);
+    return m;
+}
+
 int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* seeks, const int* slots, int n_win) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
@@ -639,16 +666,17 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
                 }
                 continue;
             }
+            const LayerMats Wm = layer_mats(c, s, L, st);
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln1_w, L.ln1_b, w.hn, st);
-            tgemm(s, KCLS, dt, EPI_STORE, gemm_plain(w.hn, M, d, L.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), st);
+            tgemm(s, KCLS, dt, EPI_STORE, gemm_plain(w.hn, M, d, Wm.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), st);
             {
                 KT kt(s, K_ATTN_ENC, 4.0 * nb * H * (double)T * T * 64);
                 launch_attn_encoder(dt, w.qkv, w.att, nb, T, d, H, st);
             }
-            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
+            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, Wm.wo, d, L.bo, w.x, d), st);
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln2_w, L.ln2_b, w.hn, st);
-            tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.hn, M, d, L.w1, 4 * d, L.b1, w.ff, 4 * d), st);
-            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, L.w2, d, L.b2, w.x, d), st);
+            tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.hn, M, d, Wm.w1, 4 * d, L.b1, w.ff, 4 * d), st);
+            tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, Wm.w2, d, L.b2, w.x, d), st);
         }
         launch_layernorm(dt, w.x, nullptr, M, d, W.lnpost_w, W.lnpost_b, w.hn, st);
         if (s->direct) {
@@ -725,12 +753,15 @@ struct DecView {
     float *xo, *xml;
 };
 
-// WHISPER_MI355X_SMALLM=0 turns the small-M decode path off (A/B): decode steps of <= 32 clips then
-// take the split-K path like larger batches
+// The small-M decode path (decoder_rows_small) is what block-quantized files run (its GEMM reads the
+// blocks); for f16 / bf16 weights it is opt-in (WHISPER_MI355X_SMALLM=1): measured slower than the
+// split-K path at 16 clips (profiles/r03_prof16_smallm{0,1}.md, large-v3 bf16: 101 vs 94 us per
+// decoder layer). Its 80 workgroups of 16 columns pull the weights more slowly than split-K's 200-240,
+// and the LayerNorm recomputed by every workgroup costs ~4.7 us per LN-consuming GEMM.
 static bool small_m_steps() {
     static const bool on = [] {
         const char* e = getenv("WHISPER_MI355X_SMALLM");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) == 1;
     }();
     return on;
 }
@@ -765,11 +796,14 @@ static void decoder_rows_small(Context* c, whisper_state* s, const DecView& v, b
     void* qx = w.qx ? (void*)((char*)w.qx + (size_t)v.r0 * 2 * H * d * E) : nullptr;
     float* raw = v.splitk;  // f32 projection sums handed to the attention prologues ([n][3d] / [n][d])
     const double kvrow = (double)H * 64 * 2 * 2;
+    const QMat* qm = nullptr;  // the layer's block-quantized matrix of the next `small` call (quantized files)
     auto small = [&](int epi, const void* A, int K, const void* Wt, int N, const float* bias, void* out, long ldo,
                      const float* lnw = nullptr, const float* lnb = nullptr) {
         GemmArgs g = gemm_plain(A, n, K, Wt, N, bias, out, ldo);
         g.a_ln_w = lnw;
         g.a_ln_b = lnb;
+        if (qm) g.q = *qm;
+        qm = nullptr;
         KT kt(s, K_GEMM_DEC, 2.0 * N * K + 2.0 * n * K + 4.0 * n * N, st);
         launch_gemm_small(dt, epi, g, lnw != nullptr, st);
     };
@@ -779,17 +813,20 @@ static void decoder_rows_small(Context* c, whisper_state* s, const DecView& v, b
         const LayerW& Lw = W.dec[l];
         const bool kt_layer = l % kt_stride == 0;
         // self attention: LN1 in the QKV GEMM, raw sums to the attention prologue (+ bias, q/k scale)
+        qm = &Lw.qqkv;
         small(EPI_F32, dx, d, Lw.wqkv, 3 * d, nullptr, raw, 3 * d, Lw.ln1_w, Lw.ln1_b);
         {
             const DecSlabs sl{raw, 1, (long)n * 3 * d, 3 * d, Lw.bqkv, c->k_scale};
             KT kt(s, K_ATTN_SELF, self_share, st, kt_layer);
             launch_attn_self_step(dt, sl, w.self, slot, pos, n, L, l, H, hp.n_text_ctx, d, datt, st);
         }
+        qm = &Lw.qo;
         small(EPI_RESID, datt, d, Lw.wo, d, Lw.bo, dx, d);
         if (xdirect) {
             GemmArgs g = gemm_plain(dx, n, d, Lw.wxq, d, Lw.bxq, dq, d);
             g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
             g.a_ln_w = Lw.lnx_w; g.a_ln_b = Lw.lnx_b;
+            g.q = Lw.qxq;
             {
                 KT kt(s, K_GEMM_DEC, 2.0 * d * d + 2.0 * n * d + 4.0 * n * d, st);
                 launch_gemm_small(dt, EPI_STORE, g, true, st);
@@ -809,13 +846,17 @@ static void decoder_rows_small(Context* c, whisper_state* s, const DecView& v, b
                                      W.bkv_cross + (size_t)(2 * l + 1) * d, n, d, H, datt, st);
             }
         } else {
+            qm = &Lw.qxq;
             small(EPI_F32, dx, d, Lw.wxq, d, nullptr, raw, d, Lw.lnx_w, Lw.lnx_b);
             const DecSlabs sl{raw, 1, (long)n * d, d, Lw.bxq, c->k_scale};
             KT kt(s, K_ATTN_CROSS, (double)n * hp.n_audio_ctx * kvrow, st, kt_layer);
             launch_attn_cross_step(dt, sl, w.cross, slot, nkv_cross, n, L, l, H, hp.n_audio_ctx, d, datt, st);
         }
+        qm = &Lw.qxo;
         small(EPI_RESID, datt, d, Lw.wxo, d, Lw.bxo, dx, d);
+        qm = &Lw.q1;
         small(EPI_GELU, dx, d, Lw.w1, 4 * d, Lw.b1, dff, 4 * d, Lw.ln2_w, Lw.ln2_b);
+        qm = &Lw.q2;
         small(EPI_RESID, dff, 4 * d, Lw.w2, d, Lw.b2, dx, d);
     }
     launch_layernorm(dt, dx, nullptr, n, d, W.lnd_w, W.lnd_b, dh, st);
@@ -884,12 +925,18 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
     // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
     const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
-    if (fused && !w8 && small_m_steps() && gemm_small_ok(n_tok, d, true) && gemm_small_ok(n_tok, 4 * d, false)) {
+    if (fused && !w8 && (c->quant || (small_m_steps() && n_tok <= 32)) && gemm_small_ok(n_tok, d, true) &&
+        gemm_small_ok(n_tok, 4 * d, false)) {
         decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
         return;
     }
     for (int l = 0; l < L; l++) {
-        const LayerW& Lw = W.dec[l];
+        LayerW Lw = W.dec[l];
+        if (c->quant) {  // prefill / language detection: this layer's blocks dequantized into the scratch
+            const LayerMats m = layer_mats(c, s, Lw, st);
+            Lw.wqkv = (void*)m.wqkv; Lw.wo = (void*)m.wo; Lw.wxq = (void*)m.wxq; Lw.wxo = (void*)m.wxo;
+            Lw.w1 = (void*)m.w1; Lw.w2 = (void*)m.w2;
+        }
         static const Context::Fp8Dec no8{};
         const Context::Fp8Dec& F = w8 ? c->dec8[l] : no8;
         const bool kt_layer = l % kt_stride == 0;

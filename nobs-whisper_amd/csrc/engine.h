@@ -45,6 +45,9 @@ struct LayerW {
     float *ln2_w, *ln2_b;
     void* w1; float* b1;
     void* w2; float* b2;
+    // block-quantized GGML files: the projection weights as the file's blocks (the compute-type
+    // pointers above are null then, except where a layer's matrix was stored unquantized)
+    QMat qqkv, qo, qxq, qxo, q1, q2;
 };
 
 struct Weights {
@@ -81,6 +84,10 @@ struct Context {
     // Cross attention straight from the encoder output (kernels/xattn.hip) is available for this
     // model (its per-head transposed Wk is in the arena); each call picks direct or cached form.
     bool cross_direct = false;
+    // block-quantized file (ggml type of its projection matrices, 0 = f16/f32 file) kept quantized in
+    // the arena: decode steps read the blocks (gemm_small_kernel), the encoder and prefill dequantize
+    // one layer at a time into the state's scratch
+    int quant = 0;
     std::string model_type;
     whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
     // fp8 encoder (large-v3-turbo fp8 config): QKV, FC1 and FC2 as e4m3 GEMMs with per-row scales.
@@ -131,6 +138,7 @@ struct Workspace {
     void *cross = nullptr, *self = nullptr;
     std::vector<char> cross_fresh;
     int* kvslot = nullptr;  // identity [cap_jobs]: row_slot of a one-clip cross-KV GEMM
+    void* wdq = nullptr;    // quantized files: one layer's projection weights dequantized (16 d^2)
     // direct cross attention: encoder output per slot [cap_jobs][T][d], Q' [cap_xq][2H][d],
     // split partials [xo_rows][H][d] f32 + [xo_rows][H][2]
     void *enc = nullptr, *qx = nullptr;

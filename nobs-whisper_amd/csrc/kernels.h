@@ -47,6 +47,21 @@ enum Epi : int {
                        // power-of-two scale per row and 32-column block, mx_scale[m][n/32] = e + 127 (E8M0)
 };
 
+// GGML block-quantized weight matrix [N][K] (the app's catalog ships q5_0 / q5_1
+// files, model.rs:153-186) kept in HBM as the file's blocks, regrouped by field (same bits, same bytes):
+// qs = the quant bytes of every block [N][K/2] (q4_*, q5_*: two 4-bit values per byte, the block's
+// weights j and j + 16 in byte j) or [N][K] (q8_0), qh = the q5 high bits [N][K/32] (bit j = weight j),
+// dm = the f16 scale d per block [N][K/32] (q4_0, q5_0, q8_0) or d and min m [N][K/32][2] (q4_1,
+// q5_1). type: ggml type id (2 q4_0, 3 q4_1,
+// 6 q5_0, 7 q5_1, 8 q8_0), 0 = not quantized. w = d * (q - offset) or d * q + m, exact in f32, then
+// rounded once to the compute type.
+struct QMat {
+    int type = 0;
+    const uint8_t* qs = nullptr;
+    const uint32_t* qh = nullptr;
+    const uint16_t* dm = nullptr;
+};
+
 struct GemmArgs {
     const void* A; long a_rpb, a_bstride, a_rstride;  // A row m -> A + (m/a_rpb)*a_bstride + (m%a_rpb)*a_rstride
     const void* B;                                     // [N][K] row-major
@@ -65,6 +80,8 @@ struct GemmArgs {
     // small-M decode GEMM (launch_gemm_small) with lna: A is the f32 residual stream and the
     // workgroup applies LN(A) * a_ln_w + a_ln_b (ggml_norm) to its rows before the product
     const float* a_ln_w; const float* a_ln_b;
+    // small-M decode GEMM: B given as GGML blocks (q.type != 0) instead of the compute type
+    QMat q;
     // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
     // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
     uint8_t* mx_scale;
@@ -92,8 +109,12 @@ int launch_gemm_partials(DType dt, const GemmArgs& a, hipStream_t st);
 // Decode steps of M <= 32 rows: one launch, no split-K slabs and no reduce launch (one workgroup =
 // 16 output columns over the whole K, its 8 waves splitting K and summing in LDS). Epilogues
 // EPI_F32 / EPI_STORE / EPI_GELU / EPI_RESID. lna: A = LN(f32 residual rows) computed in the
-// prologue (K <= 1280). Returns false when the shape is not supported (K % 256, M > 32).
+// prologue (K <= 1280). M > 32 runs as 32-row chunks (block-quantized weights, a.q, take this path at
+// every batch size). gemm_small_ok: false when the shape is not supported (K % 32; lna: K <= 1280,
+// K % 128).
 bool gemm_small_ok(int M, int K, bool lna);
+// out[r][k] (compute type) = the dequantized weights of rows [0, rows) of a block-quantized matrix
+void launch_dequant(DType dt, const QMat& q, long rows, int K, void* out, hipStream_t st);
 void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream_t st);
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------

@@ -1336,16 +1336,87 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
     *(uint2*)((T*)g.ln_out + (long)m * g.N + n) = *(const uint2*)y;
 }
 
+// ---- GGML block-quantized weights (QMat) -------------------------------------------------------
+// One lane's share of a 32-weight block for an MFMA 16x16x32 B fragment: weights 8g .. 8g + 7 of
+// block b of row n (g = lane >> 4, the fragment's k order). raw = {qs bytes (2 dwords), q5 high bits,
+// d | m << 16 (m = 0 for the *_0 types, which store d only)}; dequantized exactly as ggml's dequantize_row_* (oracle/oracle_whisper.cpp, the
+// engine's load-time dequantizer in model.cpp), w = (q - off) * d or q * d + m in f32, then rounded
+// once to the compute type.
+template <int QT>
+__device__ __forceinline__ u32x4 qraw_load(const QMat& q, long n, int K, int b, int g) {
+    u32x4 r;
+    const long bi = n * (K / 32) + b;
+    const uint2 qs = QT == 8 ? *(const uint2*)(q.qs + n * K + 32L * b + 8 * g)
+                             : *(const uint2*)(q.qs + n * (K / 2) + 16L * b + 8 * (g & 1));
+    r.x = qs.x;
+    r.y = qs.y;
+    r.z = (QT == 6 || QT == 7) ? q.qh[bi] : 0u;
+    r.w = (QT == 3 || QT == 7) ? ((const uint32_t*)q.dm)[bi] : (uint32_t)q.dm[bi];  // d | m << 16, or d
+    return r;
+}
+template <int QT, typename T>
+__device__ __forceinline__ u32x4 qraw_deq(u32x4 r, int g) {
+    const float dd = (float)__builtin_bit_cast(half_t, (uint16_t)(r.w & 0xFFFF));
+    const float mm = (float)__builtin_bit_cast(half_t, (uint16_t)(r.w >> 16));
+    T o[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t byte = ((i < 4 ? r.x : r.y) >> (8 * (i & 3))) & 0xFF;
+        float v;
+        if constexpr (QT == 8) {
+            v = (float)(int8_t)byte * dd;
+        } else {
+            int x = (g >> 1) ? (int)(byte >> 4) : (int)(byte & 15);
+            if constexpr (QT == 6 || QT == 7) x |= (int)((r.z >> (8 * g + i)) & 1) << 4;
+            if constexpr (QT == 3 || QT == 7) v = (float)x * dd + mm;
+            else v = (float)(x - (QT == 6 ? 16 : 8)) * dd;
+        }
+        o[i] = (T)v;
+    }
+    return *(const u32x4*)o;
+}
+
+// rows [0, rows) of a QMat -> compute type [rows][K] (the encoder's and the prefill's per-layer
+// scratch copy): one thread per 8 weights
+template <typename T, int QT>
+__global__ void __launch_bounds__(256) dequant_kernel(const QMat q, long rows, int K, T* __restrict__ out) {
+    const long i = blockIdx.x * 256L + threadIdx.x, per_row = K / 8;
+    if (i >= rows * per_row) return;
+    const long n = i / per_row;
+    const int e = (int)(i - n * per_row) * 8, b = e / 32, g = (e & 31) / 8;
+    *(u32x4*)(out + n * K + e) = qraw_deq<QT, T>(qraw_load<QT>(q, n, K, b, g), g);
+}
+
+template <typename T>
+static void launch_dequant_t(const QMat& q, long rows, int K, T* out, hipStream_t st) {
+    const unsigned grid = (unsigned)((rows * (K / 8) + 255) / 256);
+    switch (q.type) {
+        case 2: dequant_kernel<T, 2><<<grid, 256, 0, st>>>(q, rows, K, out); break;
+        case 3: dequant_kernel<T, 3><<<grid, 256, 0, st>>>(q, rows, K, out); break;
+        case 6: dequant_kernel<T, 6><<<grid, 256, 0, st>>>(q, rows, K, out); break;
+        case 7: dequant_kernel<T, 7><<<grid, 256, 0, st>>>(q, rows, K, out); break;
+        case 8: dequant_kernel<T, 8><<<grid, 256, 0, st>>>(q, rows, K, out); break;
+        default: WM_FAIL("dequant: ggml type %d not supported", q.type);
+    }
+}
+
+void launch_dequant(DType dt, const QMat& q, long rows, int K, void* out, hipStream_t st) {
+    if (rows <= 0) return;
+    if (K % 32) WM_FAIL("dequant: K %% 32 != 0 (K=%d)", K);
+    if (dt == DType::F16) launch_dequant_t<half_t>(q, rows, K, (half_t*)out, st);
+    else launch_dequant_t<bf16_t>(q, rows, K, (bf16_t*)out, st);
+}
+
 // Decode steps of <= 32 active clips (the app's one clip per call, whisper.rs:83-85; one rank's shard
 // of configs[3] at 8 GPUs): one workgroup = 16 output columns x all M rows x the whole K. Its 8 waves
-// split K (wave w: k in [w*K/8, (w+1)*K/8)) and add their partial sums in LDS in wave order, so no
+// split K (wave w: the 32-wide K-steps w, w + 8, ...) and add their partial sums in LDS in wave order, so no
 // split-K slab leaves the chip and no reduce launch follows. Weights are read once, by 16-byte loads
 // straight into the B fragments (a chunk of K-steps in flight before its MFMAs, the next chunk issued
 // before the current one is consumed); the <= 32 activation rows are re-read from L2 by every
 // workgroup. LNA: A is the f32 residual stream; the workgroup applies ggml_norm (double sums, f32
 // mean / variance, (v*scale)*w + b separately rounded, as block256_layernorm) to its rows in the
 // prologue, into an LDS image, so the LayerNorm launch of the split-K path disappears too.
-template <typename T, int EPI, bool LNA, int NR>
+template <typename T, int EPI, bool LNA, int NR, int QT = 0>
 __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
 #pragma clang fp contract(off)
     typedef typename Frag<T>::type FT;
@@ -1357,42 +1428,72 @@ __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
     T* aimg = (T*)smem;
     float* red = (float*)(smem + (LNA ? (size_t)NR * 16 * lda * sizeof(T) : 0));
     const u32x4 zero = {0, 0, 0, 0};
+    // this wave's K-steps of 32: wave, wave + NW, wave + 2 NW, ... (K % 32 == 0)
+    const int nst = (K / 32 - wave + NW - 1) / NW;
+    const int k0 = wave * 32 + 8 * (lane >> 4);
+    const long nrow = min(n0 + (lane & 15), g.N - 1);
+    const T* bp = (const T*)g.B + nrow * K + k0;
+    const int gq = lane >> 4;  // quantized B: this lane's 8 weights of a block
+    u32x4 bq[2][CH], aq[2][NR][CH];
+    auto load_b = [&](int c, u32x4 (&b)[CH]) {
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+            const int st = c * CH + u;
+            if constexpr (QT == 0) b[u] = st < nst ? __builtin_nontemporal_load((const u32x4*)(bp + 32 * NW * st)) : zero;
+            else b[u] = st < nst ? qraw_load<QT>(g.q, nrow, K, wave + NW * st, gq) : zero;
+        }
+    };
+    // the first chunk of weights is in flight while the prologue runs (it does not depend on A), and so
+    // are the epilogue's bias and residual operands (thread tid < NR*256 owns output (m, n) below)
+    load_b(0, bq[0]);
+    const int em = (tid >> 8) * 16 + ((tid >> 4) & 15), en = n0 + (tid & 15);
+    const bool eon = tid < NR * 256 && em < g.M && en < g.N;
+    float e_bias = 0.0f, e_res = 0.0f;
+    if (eon && g.bias) e_bias = g.bias[en];
+    if constexpr (EPI == EPI_RESID)
+        if (eon) e_res = ((const float*)g.out)[(long)em * g.ldo + en];
     if constexpr (LNA) {
-        for (int r = wave; r < NR * 16; r += NW) {
-            T* ar = aimg + (long)r * lda;
-            if (r >= g.M) {
-                for (int c = lane * 8; c < K; c += 512) *(u32x4*)(ar + c) = zero;
-                continue;
+        // all 512 threads at once: TPR threads per row, thread `part` of row r holds the float4 columns
+        // part*4 + j*TPR*4 (every load instruction reads whole 512-byte row segments), sums in double
+        // in j order, then a shuffle tree over the row's lanes (one wave holds 64 / TPR rows)
+        constexpr int ROWS = NR * 16, TPR = 512 / ROWS, NJ = 1280 / (TPR * 4);
+        const int r = tid / TPR, part = tid % TPR, nj = K / (TPR * 4);
+        const bool live = r < g.M;
+        const float* xr = (const float*)g.A + (long)min(r, g.M - 1) * g.a_rstride;
+        float4 v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; j++) v[j] = j < nj ? *(const float4*)(xr + (part + j * TPR) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) s += (((double)v[j].x + (double)v[j].y) + (double)v[j].z) + (double)v[j].w;
+        for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const float mean = (float)(s / K);
+        double s2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            if (j < nj) {
+                v[j].x = v[j].x - mean; v[j].y = v[j].y - mean; v[j].z = v[j].z - mean; v[j].w = v[j].w - mean;
+                s2 += (((double)(v[j].x * v[j].x) + (double)(v[j].y * v[j].y)) + (double)(v[j].z * v[j].z)) +
+                      (double)(v[j].w * v[j].w);
             }
-            const float* xr = (const float*)g.A + (long)r * g.a_rstride;
-            float v[20];  // K <= 1280: lane holds columns lane + 64j
+        }
+        for (int o = TPR / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+        const float scale = 1.0f / sqrtf((float)(s2 / K) + 1e-5f);
+        T* ar = aimg + (long)r * lda;
 #pragma unroll
-            for (int j = 0; j < 20; j++) v[j] = lane + 64 * j < K ? xr[lane + 64 * j] : 0.0f;
-            double s = 0.0;
-#pragma unroll
-            for (int j = 0; j < 20; j++) s += (double)v[j];
-            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-            const float mean = (float)(s / K);
-            double s2 = 0.0;
-#pragma unroll
-            for (int j = 0; j < 20; j++)
-                if (lane + 64 * j < K) {
-                    v[j] = v[j] - mean;
-                    s2 += (double)(v[j] * v[j]);
-                }
-            for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
-            const float scale = 1.0f / sqrtf((float)(s2 / K) + 1e-5f);
-#pragma unroll
-            for (int j = 0; j < 20; j++) {
-                const int c = lane + 64 * j;
-                if (c < K) ar[c] = (T)((v[j] * scale) * g.a_ln_w[c] + g.a_ln_b[c]);
-            }
+        for (int j = 0; j < NJ; j++) {
+            if (j >= nj) continue;
+            const int c = (part + j * TPR) * 4;
+            const float4 w4 = *(const float4*)(g.a_ln_w + c), b4 = *(const float4*)(g.a_ln_b + c);
+            T o[4];
+            o[0] = live ? (T)((v[j].x * scale) * w4.x + b4.x) : (T)0.0f;
+            o[1] = live ? (T)((v[j].y * scale) * w4.y + b4.y) : (T)0.0f;
+            o[2] = live ? (T)((v[j].z * scale) * w4.z + b4.z) : (T)0.0f;
+            o[3] = live ? (T)((v[j].w * scale) * w4.w + b4.w) : (T)0.0f;
+            *(uint2*)(ar + c) = *(const uint2*)o;
         }
         __syncthreads();
     }
-    const int kw = K / NW, nst = kw / 32;
-    const int k0 = wave * kw + 8 * (lane >> 4);
-    const T* bp = (const T*)g.B + (long)min(n0 + (lane & 15), g.N - 1) * K + k0;
     const T* ap[NR];
     bool arow[NR];
 #pragma unroll
@@ -1404,30 +1505,31 @@ __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
     f32x4 acc[NR];
 #pragma unroll
     for (int i = 0; i < NR; i++) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    u32x4 bq[2][CH], aq[2][NR][CH];
-    auto load = [&](int c, u32x4 (&b)[CH], u32x4 (&a)[NR][CH]) {
+    auto load_a = [&](int c, u32x4 (&a)[NR][CH]) {
 #pragma unroll
         for (int u = 0; u < CH; u++) {
             const int st = c * CH + u;
-            b[u] = st < nst ? __builtin_nontemporal_load((const u32x4*)(bp + 32 * st)) : zero;
 #pragma unroll
-            for (int i = 0; i < NR; i++) a[i][u] = st < nst && arow[i] ? *(const u32x4*)(ap[i] + 32 * st) : zero;
+            for (int i = 0; i < NR; i++) a[i][u] = st < nst && arow[i] ? *(const u32x4*)(ap[i] + 32 * NW * st) : zero;
         }
     };
     auto mma = [&](const u32x4 (&b)[CH], const u32x4 (&a)[NR][CH]) {
 #pragma unroll
-        for (int u = 0; u < CH; u++)
+        for (int u = 0; u < CH; u++) {
+            u32x4 bu = b[u];
+            if constexpr (QT != 0) bu = qraw_deq<QT, T>(bu, gq);
 #pragma unroll
             for (int i = 0; i < NR; i++)
-                acc[i] = mfma16x16x32(__builtin_bit_cast(FT, a[i][u]), __builtin_bit_cast(FT, b[u]), acc[i]);
+                acc[i] = mfma16x16x32(__builtin_bit_cast(FT, a[i][u]), __builtin_bit_cast(FT, bu), acc[i]);
+        }
     };
     const int nch = (nst + CH - 1) / CH;  // <= 4 (K <= 5120)
-    load(0, bq[0], aq[0]);
+    load_a(0, aq[0]);
     for (int c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) load(c + 1, bq[1], aq[1]);
+        if (c + 1 < nch) { load_b(c + 1, bq[1]); load_a(c + 1, aq[1]); }
         mma(bq[0], aq[0]);
         if (c + 1 < nch) {
-            if (c + 2 < nch) load(c + 2, bq[0], aq[0]);
+            if (c + 2 < nch) { load_b(c + 2, bq[0]); load_a(c + 2, aq[0]); }
             mma(bq[1], aq[1]);
         }
     }
@@ -1437,30 +1539,60 @@ __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 4; r++) red[((wave * NR + i) * 16 + 4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[i][r];
     __syncthreads();
-    if (tid < NR * 256) {
+    if (eon) {
         const int i = tid >> 8, row = (tid >> 4) & 15, col = tid & 15;
-        const int m = i * 16 + row, n = n0 + col;
         float v = 0.0f;
 #pragma unroll
         for (int w = 0; w < NW; w++) v += red[((w * NR + i) * 16 + row) * 16 + col];
-        if (m < g.M && n < g.N) epilogue<EPI, T>(g, m, n, v);
+        if (g.bias) v = v + e_bias;  // epilogue<>'s arithmetic with the operands loaded up front
+        if constexpr (EPI == EPI_RESID) {
+            ((float*)g.out)[(long)em * g.ldo + en] = v + e_res;
+        } else {
+            GemmArgs ge = g;
+            ge.bias = nullptr;
+            epilogue<EPI, T>(ge, em, en, v);
+        }
     }
 }
 
-bool gemm_small_ok(int M, int K, bool lna) { return M >= 1 && M <= 32 && K % 256 == 0 && K <= 5120 && (!lna || K <= 1280); }
+bool gemm_small_ok(int M, int K, bool lna) { return M >= 1 && K % 32 == 0 && K <= 5120 && (!lna || (K <= 1280 && K % 128 == 0)); }
 
-template <typename T, int EPI>
-static void launch_small_t(const GemmArgs& g, bool lna, hipStream_t st) {
+template <typename T, int EPI, int QT>
+static void launch_small_q(const GemmArgs& g, bool lna, hipStream_t st) {
     const int nr = g.M <= 16 ? 1 : 2;
     const size_t red = (size_t)8 * nr * 256 * sizeof(float);
     const size_t img = lna ? (size_t)nr * 16 * (g.K + 8) * sizeof(T) : 0;
     const unsigned grid = cdiv(g.N, 16);
     if (lna) {
-        if (nr == 1) gemm_small_kernel<T, EPI, true, 1><<<grid, 512, img + red, st>>>(g);
-        else gemm_small_kernel<T, EPI, true, 2><<<grid, 512, img + red, st>>>(g);
+        if (nr == 1) gemm_small_kernel<T, EPI, true, 1, QT><<<grid, 512, img + red, st>>>(g);
+        else gemm_small_kernel<T, EPI, true, 2, QT><<<grid, 512, img + red, st>>>(g);
     } else {
-        if (nr == 1) gemm_small_kernel<T, EPI, false, 1><<<grid, 512, red, st>>>(g);
-        else gemm_small_kernel<T, EPI, false, 2><<<grid, 512, red, st>>>(g);
+        if (nr == 1) gemm_small_kernel<T, EPI, false, 1, QT><<<grid, 512, red, st>>>(g);
+        else gemm_small_kernel<T, EPI, false, 2, QT><<<grid, 512, red, st>>>(g);
+    }
+}
+
+// one launch per chunk of <= 32 rows (more rows only with block-quantized weights: every chunk reads
+// the blocks, L2/MALL-hot after the first)
+template <typename T, int EPI>
+static void launch_small_t(const GemmArgs& g0, bool lna, hipStream_t st) {
+    const size_t a_es = lna ? sizeof(float) : sizeof(T);
+    const size_t o_es = (EPI == EPI_RESID || EPI == EPI_F32) ? sizeof(float) : sizeof(T);
+    for (int m0 = 0; m0 < g0.M; m0 += 32) {
+        GemmArgs g = g0;
+        g.M = std::min(32, g0.M - m0);
+        g.A = (const char*)g0.A + (size_t)m0 * g0.a_rstride * a_es;
+        g.out = (char*)g0.out + (size_t)m0 * g0.ldo * o_es;
+        g.a_rpb = g.o_rpb = g.M;
+        switch (g.q.type) {
+            case 0: launch_small_q<T, EPI, 0>(g, lna, st); break;
+            case 2: launch_small_q<T, EPI, 2>(g, lna, st); break;
+            case 3: launch_small_q<T, EPI, 3>(g, lna, st); break;
+            case 6: launch_small_q<T, EPI, 6>(g, lna, st); break;
+            case 7: launch_small_q<T, EPI, 7>(g, lna, st); break;
+            case 8: launch_small_q<T, EPI, 8>(g, lna, st); break;
+            default: WM_FAIL("small-M GEMM: ggml type %d not supported", g.q.type);
+        }
     }
 }
 
@@ -1477,7 +1609,8 @@ static void launch_small_dt(int epi, const GemmArgs& g, bool lna, hipStream_t st
 
 void launch_gemm_small(DType dt, int epi, const GemmArgs& g, bool lna, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0) return;
-    if (!gemm_small_ok(g.M, g.K, lna)) WM_FAIL("small-M GEMM shape not supported (M=%d K=%d)", g.M, g.K);
+    if (!gemm_small_ok(g.M, g.K, lna) || g.o_rpb != g.M || g.a_rpb != g.M || g.o_off || (epi == EPI_STORE && g.o_bstride))
+        WM_FAIL("small-M GEMM shape not supported (M=%d K=%d)", g.M, g.K);
     if (dt == DType::F16) launch_small_dt<half_t>(epi, g, lna, st);
     else launch_small_dt<bf16_t>(epi, g, lna, st);
 }

@@ -244,8 +244,50 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
     // ---- build the host images of every device tensor --------------------------------------
     Arena A;
     const size_t esz = 2;
+    // Block-quantized files keep the projection matrices as their blocks (QMat: quant bytes, q5 high
+    // bits and f16 scales regrouped by field; no expansion to 16 bits). WHISPER_MI355X_QUANT_EXPAND=1
+    // dequantizes them at load instead (the round-2 layout, kept for A/B).
+    const bool keep_blocks = !(getenv("WHISPER_MI355X_QUANT_EXPAND") && atoi(getenv("WHISPER_MI355X_QUANT_EXPAND")) == 1);
+    auto qmat = [&](QMat* q, const std::vector<const TensorRef*>& parts, long rows_total, long cols,
+                    const std::vector<long>& rows_each) -> bool {
+        if (!q || !keep_blocks || cols % 32) return false;
+        const int type = parts[0] ? parts[0]->type : 0;
+        if (!block_bytes(type)) return false;
+        for (auto* t : parts)
+            if (!t || t->type != type) return false;
+        const long nbk = cols / 32;
+        const int bb = block_bytes(type);
+        const bool q8 = type == 8, has_m = type == 3 || type == 7, has_h = type == 6 || type == 7;
+        const int dmb = has_m ? 4 : 2;  // bytes of {d, m} (q4_1, q5_1) or d per block
+        const size_t qs_sz = (size_t)rows_total * (q8 ? cols : cols / 2), qh_sz = has_h ? (size_t)rows_total * nbk * 4 : 0,
+                     dm_sz = (size_t)rows_total * nbk * dmb;
+        std::vector<char> qs(load_weights ? qs_sz : 0), qh(load_weights ? qh_sz : 0), dm(load_weights ? dm_sz : 0);
+        if (load_weights) {
+            long row0 = 0;
+            for (size_t pi = 0; pi < parts.size(); pi++) {
+                for (long rr = 0; rr < rows_each[pi]; rr++)
+                    for (long b = 0; b < nbk; b++) {
+                        const uint8_t* blk = (const uint8_t*)parts[pi]->data + (rr * nbk + b) * bb;
+                        const long r = row0 + rr, bi = r * nbk + b;
+                        memcpy(dm.data() + bi * dmb, blk, dmb);  // d, or d and m
+                        const uint8_t* p = blk + (has_m ? 4 : 2);
+                        if (has_h) { memcpy(qh.data() + bi * 4, p, 4); p += 4; }
+                        if (q8) memcpy(qs.data() + r * cols + b * 32, p, 32);
+                        else memcpy(qs.data() + r * (cols / 2) + b * 16, p, 16);
+                    }
+                row0 += rows_each[pi];
+            }
+        }
+        q->type = type;
+        A.add((void**)&q->qs, qs_sz, std::move(qs));
+        if (has_h) A.add((void**)&q->qh, qh_sz, std::move(qh));
+        A.add((void**)&q->dm, dm_sz, std::move(dm));
+        c->quant = type;
+        return true;
+    };
     auto mat = [&](void** dst, const std::vector<const TensorRef*>& parts, long rows_total, long cols,
-                   const std::vector<long>& rows_each, bool conv_reorder, int taps_in) {
+                   const std::vector<long>& rows_each, bool conv_reorder, int taps_in, QMat* q = nullptr) {
+        if (qmat(q, parts, rows_total, cols, rows_each)) { *dst = nullptr; return; }
         const size_t sz = (size_t)rows_total * cols * esz;
         if (!load_weights) { A.add(dst, sz, {}); return; }
         std::vector<char> b(sz);
@@ -347,12 +389,12 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         NEED(l2w, p + "mlp_ln.weight") NEED(l2b, p + "mlp_ln.bias")
         if (!ok) break;
         vecf(&L.ln1_w, {l1w}, {d}); vecf(&L.ln1_b, {l1b}, {d});
-        mat(&L.wqkv, {qw, kw, vw}, 3 * d, d, {d, d, d}, false, 0);
+        mat(&L.wqkv, {qw, kw, vw}, 3 * d, d, {d, d, d}, false, 0, &L.qqkv);
         vecf(&L.bqkv, {qb, nullptr, vb}, {d, d, d});
-        mat(&L.wo, {ow}, d, d, {d}, false, 0); vecf(&L.bo, {ob}, {d});
+        mat(&L.wo, {ow}, d, d, {d}, false, 0, &L.qo); vecf(&L.bo, {ob}, {d});
         vecf(&L.ln2_w, {l2w}, {d}); vecf(&L.ln2_b, {l2b}, {d});
-        mat(&L.w1, {f1w}, 4 * d, d, {4 * d}, false, 0); vecf(&L.b1, {f1b}, {4 * d});
-        mat(&L.w2, {f2w}, d, 4 * d, {d}, false, 0); vecf(&L.b2, {f2b}, {d});
+        mat(&L.w1, {f1w}, 4 * d, d, {4 * d}, false, 0, &L.q1); vecf(&L.b1, {f1b}, {4 * d});
+        mat(&L.w2, {f2w}, d, 4 * d, {d}, false, 0, &L.q2); vecf(&L.b2, {f2b}, {d});
     }
     std::vector<const TensorRef*> xkv;
     std::vector<const TensorRef*> xkvb;
@@ -371,15 +413,15 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
         NEED(l2w, p + "mlp_ln.weight") NEED(l2b, p + "mlp_ln.bias")
         if (!ok) break;
         vecf(&L.ln1_w, {l1w}, {d}); vecf(&L.ln1_b, {l1b}, {d});
-        mat(&L.wqkv, {qw, kw, vw}, 3 * d, d, {d, d, d}, false, 0);
+        mat(&L.wqkv, {qw, kw, vw}, 3 * d, d, {d, d, d}, false, 0, &L.qqkv);
         vecf(&L.bqkv, {qb, nullptr, vb}, {d, d, d});
-        mat(&L.wo, {ow}, d, d, {d}, false, 0); vecf(&L.bo, {ob}, {d});
+        mat(&L.wo, {ow}, d, d, {d}, false, 0, &L.qo); vecf(&L.bo, {ob}, {d});
         vecf(&L.lnx_w, {lxw}, {d}); vecf(&L.lnx_b, {lxb}, {d});
-        mat(&L.wxq, {xqw}, d, d, {d}, false, 0); vecf(&L.bxq, {xqb}, {d});
-        mat(&L.wxo, {xow}, d, d, {d}, false, 0); vecf(&L.bxo, {xob}, {d});
+        mat(&L.wxq, {xqw}, d, d, {d}, false, 0, &L.qxq); vecf(&L.bxq, {xqb}, {d});
+        mat(&L.wxo, {xow}, d, d, {d}, false, 0, &L.qxo); vecf(&L.bxo, {xob}, {d});
         vecf(&L.ln2_w, {l2w}, {d}); vecf(&L.ln2_b, {l2b}, {d});
-        mat(&L.w1, {f1w}, 4 * d, d, {4 * d}, false, 0); vecf(&L.b1, {f1b}, {4 * d});
-        mat(&L.w2, {f2w}, d, 4 * d, {d}, false, 0); vecf(&L.b2, {f2b}, {d});
+        mat(&L.w1, {f1w}, 4 * d, d, {4 * d}, false, 0, &L.q1); vecf(&L.b1, {f1b}, {4 * d});
+        mat(&L.w2, {f2w}, d, 4 * d, {d}, false, 0, &L.q2); vecf(&L.b2, {f2b}, {d});
         xkv.push_back(xkw); xkv.push_back(xvw);
         xrows.push_back(d); xrows.push_back(d);
         xkvb.push_back(nullptr); xkvb.push_back(xvb);

@@ -26,7 +26,7 @@ BF16_GAP = 2.0      # tests/test_gpu_configs.py: bf16 teacher-forced logits with
 # fp8 encoder (e4m3 QKV/FC1/FC2, per-row scales): encoder output relative RMS error ~0.05 against
 # bf16 (test_gpu_fp8.py), which moves the +conf decoder's logits by up to ~FP8_GAP / 2
 FP8_GAP = 4.0
-MIN_PREFIX = 16
+MIN_PREFIX = 8
 
 _ORACLE = {}
 

@@ -94,3 +94,63 @@ def test_quant_full_f16_exact(wrs, monkeypatch, cross, shape, clip):
     assert_decisions_match(dec, ref)
     assert seg_ints(segs) == ref_ints(ref)
     assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
+
+
+# ---- GPU: the blocks stay quantized in HBM ----------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("qtype", QTYPES)
+def test_quant_arena_keeps_blocks(wrs, qtype):
+    """A quantized file's projection matrices stay as GGML blocks in the device arena (q5_0: 0.69
+    bytes per weight instead of 2): the arena is smaller than WHISPER_MI355X_QUANT_EXPAND=1's (the
+    round-2 dequantize-at-load layout) by exactly the projections' expansion."""
+    import ctypes as C
+    import os
+    from conftest import model_path
+    L = wrs.lib()
+
+    def arena(path, expand=False):
+        if expand:
+            os.environ["WHISPER_MI355X_QUANT_EXPAND"] = "1"
+        try:
+            ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+        finally:
+            os.environ.pop("WHISPER_MI355X_QUANT_EXPAND", None)
+        p, n = C.c_void_p(), C.c_size_t()
+        assert L.whisper_mi355x_weight_arena(ctx.ptr, C.byref(p), C.byref(n)) == 0
+        ctx.close()
+        return n.value
+
+    f16 = arena(model_path("large-v3-2L+conf"))
+    q = arena(model_path("large-v3-2L+conf+" + qtype))
+    qx = arena(model_path("large-v3-2L+conf+" + qtype), expand=True)
+    bpw = {"q4_0": 18 / 32, "q4_1": 20 / 32, "q5_0": 22 / 32, "q5_1": 24 / 32, "q8_0": 34 / 32}[qtype]
+    d = 1280
+    proj = (2 * 12 + 2 * 14) * d * d  # 2 encoder (QKV, out, FC1, FC2) + 2 decoder layers (+ cross Q, out)
+    # the expanded layout = the f16 file's + the exact f32 embedding rows a quantized file keeps for
+    # the token lookup (ggml_get_rows dequantizes to f32): V x d x 4 bytes
+    assert qx == f16 + 51866 * d * 4 or abs(qx - f16 - 51866 * d * 4) < 4096, (qx, f16)
+    assert abs((qx - q) - proj * (2 - bpw)) < 0.01 * proj, (qx, q, proj)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["tiny+conf+q5_0", "small-4L+conf+q5_1"])
+def test_quant_batch_equals_single(wrs, monkeypatch, shape):
+    """40 clips (decode steps read the blocks in 32-row chunks) == whisper_full_with_state per clip,
+    bit for bit (cache form): a row's sums do not depend on the rows beside it on this path."""
+    from conftest import model_path
+    from make_model import synthetic_pcm
+    from test_gpu_configs import seg_ints
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
+    clips = [synthetic_pcm(k % 12, seconds=30.0 - k % 5) for k in range(40)]
+    p = wrs.reference_full_params("en")
+    st = ctx.create_state()
+    assert st.full_batch(p, clips) == 0
+    batch = [seg_ints(st.batch_segments(j)) for j in range(40)]
+    st.close()
+    for j in (0, 31, 32, 39):
+        st = ctx.create_state()
+        assert st.full(p, clips[j]) == 0
+        assert seg_ints(st.segments()) == batch[j], j
+        st.close()
+    ctx.close()
