@@ -119,10 +119,22 @@ void kt_flush(whisper_state* s) {
 }
 // GEMM launch with its algorithmic work: FLOPs for encoder-side GEMMs (MFMA-bound), HBM bytes
 // (weights + activations) for decode-side GEMMs (weight-streaming)
+// Decode-step split-K slabs are stored write-through (sc1): the lines leave the XCD's L2 while the
+// GEMM runs instead of being written back at the kernel boundary before the reduce can start
+// (MI355X_MICROARCH.md price list, "boundary": + dirty bytes / 6 TB/s). Same-box A/B, large-v3 bf16:
+// decode 864 -> 824 ms per step at 128 clips, 423 -> 413 at 16 (profiles/r03_envab_slab_gelu.txt).
+// WHISPER_MI355X_SLAB_WT=0 restores write-back stores.
+static int slab_wt() {
+    static const int on = [] {
+        const char* e = getenv("WHISPER_MI355X_SLAB_WT");
+        return e && atoi(e) == 0 ? 0 : 1;
+    }();
+    return on;
+}
 static void tgemm_ws(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st, float* ws,
                      long ws_elems) {
     GemmArgs g = g0;
-    if (cls == K_GEMM_DEC) { g.splitk_ws = ws; g.splitk_ws_elems = ws_elems; }
+    if (cls == K_GEMM_DEC) { g.splitk_ws = ws; g.splitk_ws_elems = ws_elems; g.slab_wt = slab_wt(); }
     const double work = cls == K_GEMM_ENC ? 2.0 * g.M * g.N * g.K
                                           : 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N;
     KT kt(s, cls, work, st);
@@ -575,6 +587,19 @@ static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float*
     launch_gemm_fp8(s->ctx->dt, epi, g, sa, sb, st);
 }
 
+// Encoder FC1 GELU. f16 (whisper.cpp's CPU numerics, the parity mode): ggml's f16 GELU table
+// (EPI_GELU), bit-exact with the oracle. bf16: the tanh formula in f32 (EPI_GELU_F; ggml-metal, the
+// reference app's back-end (whisper.rs:40 use_gpu), evaluates GELU by formula too, and the epilogue
+// stages no 75.8 KB table per tile): encode 340 -> 336 ms per step at 128 clips
+// (profiles/r03_envab_slab_gelu.txt). WHISPER_MI355X_GELU_F=0 keeps the table in bf16 too.
+static int enc_gelu_epi(DType dt) {
+    static const bool f = [] {
+        const char* e = getenv("WHISPER_MI355X_GELU_F");
+        return !(e && atoi(e) == 0);
+    }();
+    return dt == DType::BF16 && f ? EPI_GELU_F : EPI_GELU;
+}
+
 // Projection weights of one layer in the compute type: the arena's matrices, or, for a block-quantized
 // file, the layer's blocks dequantized into the state's scratch (one layer at a time, on the stream
 // that then runs the layer: the encoder and the prefill are big-M GEMMs that read every weight many
@@ -675,7 +700,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
             }
             tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, Wm.wo, d, L.bo, w.x, d), st);
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln2_w, L.ln2_b, w.hn, st);
-            tgemm(s, KCLS, dt, EPI_GELU, gemm_plain(w.hn, M, d, Wm.w1, 4 * d, L.b1, w.ff, 4 * d), st);
+            tgemm(s, KCLS, dt, enc_gelu_epi(dt), gemm_plain(w.hn, M, d, Wm.w1, 4 * d, L.b1, w.ff, 4 * d), st);
             tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.ff, M, 4 * d, Wm.w2, d, L.b2, w.x, d), st);
         }
         launch_layernorm(dt, w.x, nullptr, M, d, W.lnpost_w, W.lnpost_b, w.hn, st);
@@ -729,6 +754,16 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, 
     }
     w.n_qtiles = nt;
     WM_CHECK(hipMemcpyAsync(w.qtiles, w.h_qtiles, (size_t)nt * sizeof(int2), hipMemcpyHostToDevice, s->stream));
+}
+
+// decode steps, direct cross attention: the cross-Q GEMM's split-K reduce fused into the Q' projection
+// (launch_xattn_qproj_slabs, bit-identical); WHISPER_MI355X_XQ_FUSED=0 restores the two launches (A/B)
+static bool xq_fused() {
+    static const bool on = [] {
+        const char* e = getenv("WHISPER_MI355X_XQ_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 // WHISPER_MI355X_XSERP=1: odd decoder layers read each clip's encoder rows in reverse order, so that
@@ -917,6 +952,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         GemmArgs g = use8(gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N), q8, sc);
         g.splitk_ws = v.splitk;
         g.splitk_ws_elems = v.splitk_elems;
+        g.slab_wt = slab_wt();
         KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
         const int splits = launch_gemm_partials(dt, g, st);
         if (splits <= 0) WM_FAIL("decode partials GEMM not applicable");
@@ -956,15 +992,21 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b, F.wo, F.so);
         if (xdirect) {
             // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
-            // -> one pass over E per clip -> split merge + Wv
-            GemmArgs g = use8(gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d), F.wxq, F.sxq);
-            g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
-            gemm(KCLS, EPI_STORE, g);
-            const int Ta = hp.n_audio_ctx, S = xattn_splits(n_tok, Ta);
-            {
+            // -> one pass over E per clip -> split merge + Wv. Decode steps: the cross-Q GEMM leaves
+            // split-K slabs that the Q' projection reduces itself (one launch fewer per layer)
+            const void* wkt_l = (const char*)W.wkT + (size_t)l * H * d * 64 * 2;
+            if (fused && xq_fused()) {
+                const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);
+                KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * d * sl.splits + 4.0 * n_tok * H * d, st);
+                launch_xattn_qproj_slabs(dt, sl, wkt_l, n_tok, d, H, c->k_scale, qx, st);
+            } else {
+                GemmArgs g = use8(gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d), F.wxq, F.sxq);
+                g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
+                gemm(KCLS, EPI_STORE, g);
                 KT kt(s, KCLS, 2.0 * d * d + 2.0 * n_tok * d + 4.0 * n_tok * H * d, st);
-                launch_xattn_qproj(dt, dq, (const char*)W.wkT + (size_t)l * H * d * 64 * 2, n_tok, d, H, c->k_scale, qx, st);
+                launch_xattn_qproj(dt, dq, wkt_l, n_tok, d, H, c->k_scale, qx, st);
             }
+            const int Ta = hp.n_audio_ctx, S = xattn_splits(n_tok, Ta);
             {
                 // the roofline class holds decode steps only (E bytes read once per clip and layer)
                 KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2, st, kt_layer);

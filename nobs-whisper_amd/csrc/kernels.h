@@ -82,6 +82,8 @@ struct GemmArgs {
     const float* a_ln_w; const float* a_ln_b;
     // small-M decode GEMM: B given as GGML blocks (q.type != 0) instead of the compute type
     QMat q;
+    // decode-step split-K slabs stored write-through (sc1) instead of write-back
+    int slab_wt;
     // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
     // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
     uint8_t* mx_scale;
@@ -157,6 +159,10 @@ int xattn_splits(int n, int Tn);
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st);
 // rev = 1: each split's 16-row tiles in reverse order (the engine alternates per decoder layer)
+// the same Q' from the cross-Q GEMM's split-K slabs (sl: q = (T)((sum_z slab + bias) * sl.scale), the
+// EPI_STORE reduce) in one launch: bit-identical to that reduce followed by launch_xattn_qproj
+void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
+                              hipStream_t st);
 void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
                        float thr, float* opart, float* ml, hipStream_t st, int rev = 0);
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,

@@ -1203,7 +1203,13 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
                 const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
                 if (m >= g.M) continue;
                 const float v = W8 ? acc[i][j][r] * wsc : acc[i][j][r];
-                if constexpr (SPLIT) g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n] = v;
+                if constexpr (SPLIT) {
+                    float* p = &g.splitk_ws[((long)blockIdx.z * g.M + m) * g.N + n];
+                    // slab_wt: write-through (sc1) slab stores, so the lines leave the XCD's L2 while the
+                    // kernel runs instead of at its end (the kernel boundary writes dirty L2 lines back)
+                    if (g.slab_wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else *p = v;
+                }
                 else epilogue<EPI, T>(g, m, n, v);
             }
         }
@@ -1790,6 +1796,7 @@ static void launch_dt(int epi, const GemmArgs& g, hipStream_t st) {
     switch (epi) {
         case EPI_STORE: launch_t<T, EPI_STORE>(g, st); break;
         case EPI_GELU: launch_t<T, EPI_GELU>(g, st); break;
+        case EPI_GELU_F: launch_t<T, EPI_GELU_F>(g, st); break;
         case EPI_RESID: launch_t<T, EPI_RESID>(g, st); break;
         case EPI_GELU_POS: launch_t<T, EPI_GELU_POS>(g, st); break;
         case EPI_F32: launch_t<T, EPI_F32>(g, st); break;

@@ -135,13 +135,75 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
         }
 }
 
+// Q' projection fused with the cross-Q GEMM's split-K reduce (decode steps): grid (H, cdiv(n, 16)),
+// 256 threads. The workgroup first reduces q_h for its 16 tokens from the slabs, exactly as
+// splitk_reduce_kernel<EPI_STORE> would (sum over splits in order from 0, + bias, * scale, rounded to
+// T), into an LDS image; then wave w computes columns [w*d/4, (w+1)*d/4) of Q'_h for the 16 tokens
+// with the same MFMA operands and order as xattn_qproj_kernel (A = Wk_h^T rows, B = q_h, K = 64):
+// the outputs are bit-identical to the reduce + qproj pair, one launch and one round trip fewer.
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_qproj_slabs_kernel(const DecSlabs sl, const T* __restrict__ wkt, int n, int d,
+                                                                int H, float scale, T* __restrict__ qx) {
+    typedef typename Frag<T>::type FT;
+    const int h = blockIdx.x, i0 = blockIdx.y * 16;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ __attribute__((aligned(16))) T qimg[16 * 64];
+    {
+        const int tk = tid >> 4, c = h * 64 + (tid & 15) * 4, i = i0 + tk;
+        T o[4] = {(T)0.0f, (T)0.0f, (T)0.0f, (T)0.0f};
+        if (i < n) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int z = 0; z < sl.splits; z++) {
+                const float4 w = *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c);
+                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+            }
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float x = vv[k];
+                if (sl.bias) x = x + sl.bias[c + k];
+                o[k] = (T)(x * sl.scale);
+            }
+        }
+        *(uint2*)&qimg[tk * 64 + (tid & 15) * 4] = *(const uint2*)o;
+    }
+    __syncthreads();
+    FT bq[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) bq[ks] = __builtin_bit_cast(FT, *(const u32x4*)&qimg[(lane & 15) * 64 + ks * 32 + 8 * (lane >> 4)]);
+    const int cpw = d / 4, c0 = wave * cpw;  // columns of this wave (multiple of 16: d % 64 == 0)
+    const int i = i0 + (lane & 15);
+    for (int mt = 0; mt < cpw / 16; mt++) {
+        const int cr = c0 + mt * 16 + (lane & 15);
+        FT af[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++)
+            af[ks] = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + cr) * 64 + ks * 32 + 8 * (lane >> 4)));
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[ks], bq[ks], acc);
+        if (i >= n) continue;
+        const int c = c0 + mt * 16 + 4 * (lane >> 4);
+        T hi[4], lo[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const float v = acc[r] * scale;
+            hi[r] = (T)v;
+            lo[r] = (T)(v - (float)hi[r]);
+        }
+        *(uint2*)(qx + ((long)i * 2 * H + h) * d + c) = *(const uint2*)hi;
+        *(uint2*)(qx + ((long)i * 2 * H + H + h) * d + c) = *(const uint2*)lo;
+    }
+}
+
 // ---- one pass over E per (clip, split) ------------------------------------------------------------
 // NW waves x CT column tiles of 32: d = NW*CT*32, H = d/64, NQ = ceil(2H/16) score column tiles.
 // AUX: cache-policy bits of the E loads (2 = non-temporal).
 template <typename T, int NW, int CT, int AUX>
 __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
                                                              const T* __restrict__ qx, int Tn, int splits, float thr,
-                                                             float* __restrict__ opart, float* __restrict__ ml, int rev) {
+                                                             float* __restrict__ opart, float* __restrict__ ml, int rev,
+                                                             int wt) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
@@ -337,7 +399,9 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         }
     }
 
-    // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2]
+    // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2]. wt: write-through (sc1) 16-byte
+    // stores, so the partials (26 MB per launch at 128 clips) leave the XCD's L2 as they are written
+    // instead of at the kernel boundary in front of the combine
     const int h = lane & 31;
     if (h < H) {
         float* o = opart + (((long)i * splits + sp) * H + h) * D;
@@ -346,7 +410,9 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int c = cw + k * 32 + 8 * g + 4 * hh;
-                *(float4*)(o + c) = make_float4(oacc[k][4 * g], oacc[k][4 * g + 1], oacc[k][4 * g + 2], oacc[k][4 * g + 3]);
+                const f32x4 v = {oacc[k][4 * g], oacc[k][4 * g + 1], oacc[k][4 * g + 2], oacc[k][4 * g + 3]};
+                if (wt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(o + c), "v"(v) : "memory");
+                else *(f32x4*)(o + c) = v;
             }
     }
     if (tid < 16 * H && (tid & 15) == 0) {
@@ -498,6 +564,17 @@ void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, 
         xattn_qproj_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
 }
 
+void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
+                              hipStream_t st) {
+    if (n <= 0) return;
+    if (d % 64 || sl.ld % 4) WM_FAIL("fused Q' projection: d %d", d);
+    dim3 grid(H, cdiv(n, 16));
+    if (dt == DType::F16)
+        xattn_qproj_slabs_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
+    else
+        xattn_qproj_slabs_kernel<bf16_t><<<grid, 256, 0, st>>>(sl, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
+}
+
 template <typename T>
 static void launch_step_t(const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits, float thr,
                           float* opart, float* ml, int rev, hipStream_t st) {
@@ -506,11 +583,13 @@ static void launch_step_t(const void* enc, const int* slot, const void* qx, int 
     // loads are non-temporal (aux = 2): 86.6 vs 102.4 us per decode launch, 3075 vs 2921 audio-s/s.
     // WHISPER_MI355X_XNT=0 restores the default cache policy (A/B).
     static const int aux = getenv("WHISPER_MI355X_XNT") ? atoi(getenv("WHISPER_MI355X_XNT")) : 2;
+    // WHISPER_MI355X_XO_WT=1: write-through partial-O stores (A/B)
+    static const int wt = getenv("WHISPER_MI355X_XO_WT") ? atoi(getenv("WHISPER_MI355X_XO_WT")) : 0;
 #define WM_XSTEP(NW_, CT_)                                                                                                \
     if (aux == 2)                                                                                                          \
-        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev); \
+        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt); \
     else                                                                                                                   \
-        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev)
+        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt)
     switch (d) {
         case 384: WM_XSTEP(4, 3); break;
         case 512: WM_XSTEP(8, 2); break;

@@ -22,7 +22,11 @@ for (M, N, K, name, epi) in [(B_WIN * 1500, 3 * d, d, "qkv", 0), (B_WIN * 1500, 
     A = rng.standard_normal((M, K)).astype(np.float16)
     B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
     bias = np.zeros(N, np.float32)
-    _, ms = _run_gemm(wrs, ctx, A, B, bias, -1, reps=5, epi=epi)
+    res = []
+    for v in [int(x) for x in os.environ.get("VARIANTS", "-1").split(",")]:
+        _, msv = _run_gemm(wrs, ctx, A, B, bias, v, reps=5, epi=epi)
+        res.append(f"v{v} {2.0 * M * N * K / msv / 1e9:.0f}")
+    ms = msv
     ta = torch.from_numpy(A).to(torch.bfloat16).cuda()
     tb = torch.from_numpy(B).to(torch.bfloat16).cuda()
     for _ in range(3):
@@ -36,5 +40,5 @@ for (M, N, K, name, epi) in [(B_WIN * 1500, 3 * d, d, "qkv", 0), (B_WIN * 1500, 
     torch.cuda.synchronize()
     tms = e0.elapsed_time(e1) / 10
     f = 2.0 * M * N * K
-    print(f"{name:9s} M={M} N={N} K={K}: engine epi{epi} {ms:.3f} ms {f / ms / 1e9:.0f} TF/s | hipBLASLt {tms:.3f} ms "
+    print(f"{name:9s} M={M} N={N} K={K}: engine epi{epi} [{', '.join(res)}] TF/s | hipBLASLt {tms:.3f} ms "
           f"{f / tms / 1e9:.0f} TF/s", flush=True)
