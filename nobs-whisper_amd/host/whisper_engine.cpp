@@ -122,8 +122,6 @@ bool build_initial_prompt(const char* vocabulary, const char* context, std::stri
     return false;
 }
 
-namespace {
-
 std::string trim(const std::string& s) {
     auto cp = decode_utf8(s);
     size_t b = 0, e = cp.size();
@@ -131,8 +129,6 @@ std::string trim(const std::string& s) {
     while (e > b && is_ws(cp[e - 1])) e--;
     return encode_utf8(cp, b, e);
 }
-
-}  // namespace
 
 std::string filter_hallucinations(const std::string& text) {
     const std::string trimmed = trim(text);

@@ -44,6 +44,8 @@ class WhisperEngine {
 std::string filter_hallucinations(const std::string& text);
 // String::from_utf8_lossy: each maximal ill-formed subsequence -> U+FFFD (segment.to_str_lossy(), whisper.rs:137)
 std::string utf8_lossy(const std::string& bytes);
+// str::trim (Unicode White_Space at both ends)
+std::string trim(const std::string& s);
 // whisper.rs:98-105 initial prompt; false = None
 bool build_initial_prompt(const char* vocabulary, const char* context, std::string* out);
 

@@ -413,6 +413,166 @@ def _engine_lib():
     return C.CDLL(ENGINE_LIB_PATH)
 
 
+def _stream_lib():
+    L = C.CDLL(ENGINE_LIB_PATH)
+    fp = C.POINTER(C.c_float)
+    L.nobs_audio_buffer_new.restype = C.c_void_p
+    L.nobs_audio_buffer_new.argtypes = [C.c_uint]
+    L.nobs_audio_buffer_free.argtypes = [C.c_void_p]
+    L.nobs_audio_buffer_push.argtypes = [C.c_void_p, fp, C.c_long]
+    L.nobs_audio_buffer_has_silence_boundary.argtypes = [C.c_void_p]
+    L.nobs_audio_buffer_take.restype = C.c_long
+    L.nobs_audio_buffer_take.argtypes = [C.c_void_p, C.c_int, fp, C.c_long]
+    L.nobs_audio_buffer_info.argtypes = [C.c_void_p, C.POINTER(C.c_long), fp]
+    L.nobs_calculate_rms.restype = C.c_float
+    L.nobs_calculate_rms.argtypes = [fp, C.c_long]
+    L.nobs_stream_new.restype = C.c_void_p
+    L.nobs_stream_new.argtypes = [C.c_void_p, C.c_uint, C.c_int, C.c_char_p, C.c_char_p, C.c_int]
+    L.nobs_stream_push.argtypes = [C.c_void_p, fp, C.c_long]
+    L.nobs_stream_stop.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+    L.nobs_stream_dispatched.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.nobs_stream_n_results.argtypes = [C.c_void_p]
+    L.nobs_stream_result.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int]
+    L.nobs_stream_errors.argtypes = [C.c_void_p]
+    L.nobs_stream_free.argtypes = [C.c_void_p]
+    return L
+
+
+def calculate_rms(x) -> float:
+    """audio.rs:364-370 through the C++ mirror (host/audio_buffer.cpp)."""
+    import numpy as np
+    a = np.ascontiguousarray(x, dtype=np.float32)
+    return float(_stream_lib().nobs_calculate_rms(a.ctypes.data_as(C.POINTER(C.c_float)), len(a)))
+
+
+class AudioBuffer:
+    """audio.rs:29-241 AudioBuffer through the C++ mirror (host/audio_buffer.cpp): same method names;
+    take_* return a float32 array or None (Rust Option)."""
+
+    def __init__(self, sample_rate: int = 48000):
+        self.L = _stream_lib()
+        self.ptr = self.L.nobs_audio_buffer_new(sample_rate)
+        if not self.ptr:
+            raise ValueError(f"unsupported sample rate {sample_rate}")
+
+    @classmethod
+    def with_sample_rate(cls, sample_rate: int):
+        return cls(sample_rate)
+
+    def push_samples(self, x):
+        import numpy as np
+        a = np.ascontiguousarray(x, dtype=np.float32)
+        self.L.nobs_audio_buffer_push(self.ptr, a.ctypes.data_as(C.POINTER(C.c_float)), len(a))
+
+    def _info(self):
+        out, nf = (C.c_long * 4)(), C.c_float()
+        self.L.nobs_audio_buffer_info(self.ptr, out, C.byref(nf))
+        return list(out), nf.value
+
+    def __len__(self):
+        return self._info()[0][0]
+
+    def is_empty(self) -> bool:
+        return len(self) == 0
+
+    @property
+    def last_speech_pos(self) -> int:
+        return self._info()[0][1]
+
+    @property
+    def overlap_len(self) -> int:
+        return self._info()[0][2]
+
+    @property
+    def noise_floor_frames(self) -> int:
+        return self._info()[0][3]
+
+    def get_noise_floor(self) -> float:
+        return self._info()[1]
+
+    def has_silence_boundary(self) -> bool:
+        return bool(self.L.nobs_audio_buffer_has_silence_boundary(self.ptr))
+
+    def _take(self, kind):
+        import numpy as np
+        info = self._info()[0]
+        out = np.zeros(info[0] + info[2] + 1, np.float32)
+        n = self.L.nobs_audio_buffer_take(self.ptr, kind, out.ctypes.data_as(C.POINTER(C.c_float)), len(out))
+        assert n >= 0, n
+        return None if (n == 0 and kind != 2) else out[:n].copy()
+
+    def take_chunk_at_silence(self):
+        return self._take(0)
+
+    def take_forced_chunk(self):
+        return self._take(1)
+
+    def take(self):
+        return self._take(2)
+
+    def __del__(self):
+        try:
+            self.L.nobs_audio_buffer_free(self.ptr)
+        except Exception:
+            pass
+
+
+class StreamingSession:
+    """state.rs's streaming recording through the C++ mirror: on_input() is one capture callback
+    (state.rs:587-606: down-mix, push, dispatch a chunk to the worker, which resamples on the GPU and
+    transcribes with the previous text as context, state.rs:122-167); stop() is state.rs:655-798
+    (join the worker, transcribe the remaining audio, split above 30 s, join with spaces, trim)."""
+
+    def __init__(self, engine: "WhisperEngine", input_rate: int, channels: int = 1, language=None,
+                 vocabulary=None, device: int = 0):
+        self.L = _stream_lib()
+        enc = lambda s: s.encode() if s is not None else None  # noqa: E731
+        self.ptr = self.L.nobs_stream_new(engine.ptr if engine is not None else None, input_rate, channels,
+                                          enc(language), enc(vocabulary), device)
+        if not self.ptr:
+            raise ValueError(f"unsupported sample rate {input_rate}")
+        self.engine = engine
+
+    def on_input(self, data) -> int:
+        import numpy as np
+        a = np.ascontiguousarray(data, dtype=np.float32)
+        return self.L.nobs_stream_push(self.ptr, a.ctypes.data_as(C.POINTER(C.c_float)), len(a))
+
+    def stop(self) -> str:
+        buf = C.create_string_buffer(1 << 20)
+        n = self.L.nobs_stream_stop(self.ptr, buf, len(buf))
+        assert n >= 0, n
+        return buf.value.decode("utf-8", "replace")
+
+    def dispatched(self) -> list:
+        n = self.L.nobs_stream_dispatched(self.ptr, None, 0)
+        out = (C.c_int * max(1, n))()
+        self.L.nobs_stream_dispatched(self.ptr, out, n)
+        return list(out)[:n]
+
+    def results(self) -> list:
+        buf = C.create_string_buffer(1 << 20)
+        r = []
+        for i in range(self.L.nobs_stream_n_results(self.ptr)):
+            assert self.L.nobs_stream_result(self.ptr, i, buf, len(buf)) >= 0
+            r.append(buf.value.decode("utf-8", "replace"))
+        return r
+
+    def errors(self) -> int:
+        return self.L.nobs_stream_errors(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.nobs_stream_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def build_initial_prompt(vocabulary, context):
     """whisper.rs:98-105 through the C++ mirror: None when the match falls through."""
     L = _engine_lib()

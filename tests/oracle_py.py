@@ -272,3 +272,120 @@ def resample(x, rate_in: int) -> np.ndarray:
     out = np.zeros(max(cap, 1), np.float32)
     n = lib().oracle_resample(_fp(x), len(x), rate_in, _fp(out), cap)
     return out[:n].copy()
+
+
+# ---- audio.rs:29-241 AudioBuffer, restated in numpy (test infrastructure) -------------------------
+# Independent of the product's C++ (nobs-whisper_amd/host/audio_buffer.cpp): every f32 sum is a
+# float32 np.cumsum (numpy accumulates sequentially, as Rust's Iterator::sum), every product and
+# constant float32.
+_F = np.float32
+
+
+def rms_f32(x) -> np.float32:
+    """audio.rs:364-370"""
+    x = np.asarray(x, dtype=np.float32)
+    if len(x) == 0:
+        return _F(0.0)
+    s = np.cumsum(x * x, dtype=np.float32)[-1]
+    return np.sqrt(_F(s) / _F(len(x)))
+
+
+class AudioBufferRef:
+    SILENCE = _F(0.01)
+    MIN_THR = _F(0.01) * _F(0.5)
+    ONE_MINUS = _F(1.0) - _F(0.95)
+
+    def __init__(self, sample_rate: int = 48000):
+        self.sr = sample_rate
+        self._parts, self._n = [], 0
+        self.last_speech_pos = 0
+        self.noise_floor = _F(0.01)
+        self.noise_floor_frames = 0
+        self.overlap = np.zeros(0, np.float32)
+
+    @property
+    def samples(self):
+        if len(self._parts) != 1:
+            self._parts = [np.concatenate(self._parts) if self._parts else np.zeros(0, np.float32)]
+        return self._parts[0]
+
+    @samples.setter
+    def samples(self, v):
+        self._parts, self._n = [v], len(v)
+
+    def push_samples(self, x):
+        x = np.asarray(x, dtype=np.float32)
+        start = self._n
+        self._parts.append(x)
+        self._n += len(x)
+        w = self.sr // 50
+        for i, off in enumerate(range(0, len(x), w)):
+            rms = rms_f32(x[off:off + w])
+            if rms < self.noise_floor * _F(0.5) and self.noise_floor_frames < 100:
+                self.noise_floor = _F(self.noise_floor * _F(0.95)) + _F(rms * self.ONE_MINUS)
+                self.noise_floor_frames += 1
+            thr = max(_F(self.noise_floor * _F(3.0)), self.MIN_THR)
+            if rms >= thr:
+                self.last_speech_pos = start + (i + 1) * w
+
+    def take(self):
+        self.last_speech_pos = 0
+        self.overlap = np.zeros(0, np.float32)
+        out, self.samples = self.samples, np.zeros(0, np.float32)
+        return out
+
+    def has_silence_boundary(self) -> bool:
+        if self._n == 0 or self.last_speech_pos == 0:
+            return False
+        return max(0, self._n - self.last_speech_pos) >= self.sr * 700 // 1000
+
+    def _emit(self, split):
+        ov = self.sr * 200 // 1000
+        chunk = np.concatenate([self.overlap, self.samples[:split]])
+        self.overlap = self.samples[max(0, split - ov):split].copy()
+        self.samples = self.samples[split:].copy()
+        return chunk
+
+    def take_chunk_at_silence(self):
+        if not self.has_silence_boundary() or self.last_speech_pos < self.sr // 2:
+            return None
+        s0 = self.last_speech_pos
+        chunk = self._emit(s0 + (self._n - s0) // 2)
+        self.last_speech_pos = 0
+        return chunk
+
+    def take_forced_chunk(self):
+        n = self._n
+        if n <= self.sr * 25:
+            return None
+        w = self.sr // 50
+        start = max(0, n - self.sr * 5)
+        q_pos, q_rms = start, np.finfo(np.float32).max
+        pos = start
+        while pos + w <= n:
+            r = rms_f32(self.samples[pos:pos + w])
+            if r < q_rms:
+                q_rms, q_pos = r, pos
+            pos += w
+        split = min(q_pos + w // 2, n)
+        if split < self.sr // 2:
+            return None
+        chunk = self._emit(split)
+        self.last_speech_pos = self.last_speech_pos - split if self.last_speech_pos > split else 0
+        return chunk
+
+
+def stream_callback_ref(buf: AudioBufferRef, data, channels: int):
+    """state.rs:587-606 on the restated buffer: returns the dispatched chunk or None."""
+    data = np.asarray(data, dtype=np.float32)
+    if channels > 1:
+        for f in range(0, len(data), channels):
+            fr = data[f:f + channels]
+            s = np.cumsum(fr, dtype=np.float32)[-1]
+            buf.push_samples(np.array([_F(s) / _F(channels)], np.float32))
+    else:
+        buf.push_samples(data)
+    c = buf.take_chunk_at_silence()
+    if c is None:
+        c = buf.take_forced_chunk()
+    return c
