@@ -756,12 +756,13 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, 
     WM_CHECK(hipMemcpyAsync(w.qtiles, w.h_qtiles, (size_t)nt * sizeof(int2), hipMemcpyHostToDevice, s->stream));
 }
 
-// decode steps, direct cross attention: the cross-Q GEMM's split-K reduce fused into the Q' projection
-// (launch_xattn_qproj_slabs, bit-identical); WHISPER_MI355X_XQ_FUSED=0 restores the two launches (A/B)
+// decode steps, direct cross attention: WHISPER_MI355X_XQ_FUSED=1 fuses the cross-Q GEMM's split-K
+// reduce into the Q' projection (launch_xattn_qproj_slabs, bit-identical). Off by default: one launch
+// fewer per layer, but decode 843 vs 823 ms per step at 128 clips (profiles/r03_envab_xq_xowt.txt)
 static bool xq_fused() {
     static const bool on = [] {
         const char* e = getenv("WHISPER_MI355X_XQ_FUSED");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     return on;
 }

@@ -38,10 +38,11 @@ def kept_token_margins(ref):
     return out_t, out_m
 
 
-def assert_diverges_only_at_close_calls(got, exp, margins, gap, min_prefix=0):
+def assert_diverges_only_at_close_calls(got, exp, margins, gap, min_confident=0):
     """got == exp up to the first difference, which must fall on a token the oracle decided by at
-    most `gap` nats; and the identical prefix is at least min(min_prefix, len(exp)) tokens long (a
-    case whose very first steps are close calls proves nothing). Returns the prefix length."""
+    most `gap` nats; and the identical prefix holds at least min(min_confident, C) tokens that the
+    oracle decided by MORE than `gap` (C = how many such tokens exp has), so that a case whose first
+    steps are all close calls cannot pass having checked nothing. Returns the prefix length."""
     n = 0
     while n < len(exp) and n < len(got) and got[n] == exp[n]:
         n += 1
@@ -51,5 +52,8 @@ def assert_diverges_only_at_close_calls(got, exp, margins, gap, min_prefix=0):
     elif n < len(exp):
         # the run ended (EOT, window end) where the oracle went on with token n: a flip of that step
         assert margins[n] <= gap, f"ended at token {n} where the oracle's margin is {margins[n]:.3f} nats (> {gap})"
-    assert n >= min(min_prefix, len(exp)), f"identical prefix {n} < {min(min_prefix, len(exp))} tokens"
+    confident = sum(1 for m in margins[:len(exp)] if m > gap)
+    covered = sum(1 for m in margins[:n] if m > gap)
+    assert covered >= min(min_confident, confident), \
+        f"identical prefix {n} holds {covered} confident tokens < {min(min_confident, confident)}"
     return n

@@ -26,7 +26,7 @@ BF16_GAP = 2.0      # tests/test_gpu_configs.py: bf16 teacher-forced logits with
 # fp8 encoder (e4m3 QKV/FC1/FC2, per-row scales): encoder output relative RMS error ~0.05 against
 # bf16 (test_gpu_fp8.py), which moves the +conf decoder's logits by up to ~FP8_GAP / 2
 FP8_GAP = 4.0
-MIN_PREFIX = 8
+MIN_CONFIDENT = 4  # tokens decided by > the gap that the identical prefix must hold
 
 _ORACLE = {}
 
@@ -110,7 +110,8 @@ def test_turbo_bf16_256_equals_two_128(wrs, monkeypatch):
 def test_turbo_fp8_b256_vs_oracle(wrs):
     """BASELINE configs[4]: large-v3-turbo with fp8 weights (e4m3 encoder GEMMs) at batch 256 (direct
     cross attention, two decode row groups); 8 spot clips against the f16-numerics oracle: identical
-    up to the first step the oracle decided by <= FP8_GAP nats, and at least MIN_PREFIX tokens."""
+    up to the first step the oracle decided by <= FP8_GAP nats; over the spot clips together at least
+    half of the oracle's tokens identical before the first divergence."""
     from conftest import model_path
     path = model_path("large-v3-turbo-2L+conf")
     seeds = [k % 64 for k in range(256)]
@@ -155,7 +156,7 @@ def test_largev3_bf16_b128_direct_vs_oracle(wrs, monkeypatch):
         ref = oracle_full("large-v3-2L+conf", seeds[j])
         exp, margins = kept_token_margins(ref)
         got = seg_tokens(st.batch_segments(j))
-        prefixes.append((j, assert_diverges_only_at_close_calls(got, exp, margins, BF16_GAP, MIN_PREFIX), len(exp)))
+        prefixes.append((j, assert_diverges_only_at_close_calls(got, exp, margins, BF16_GAP, MIN_CONFIDENT), len(exp)))
     st.close()
     ctx.close()
     print("bf16 b128 identical prefixes (clip, tokens, of):", prefixes)
