@@ -684,6 +684,31 @@ int whisper_mi355x_debug_quant_fp8(struct whisper_context* ctx, const void* x, l
         return 0;
     });
 }
+int whisper_mi355x_debug_attn_encoder(struct whisper_context* ctx, const void* qkv, int B, int T, int d, int H,
+                                      int variant, void* out, int reps, float* ms) {
+    return guarded(nullptr, [&]() -> int {
+        if (!ctx || B < 1 || T < 1 || d != 64 * H || variant < 1 || variant > 3) return -1;
+        hipSetDevice(ctx->c.device);
+        hipStream_t st;
+        WM_CHECK(hipStreamCreate(&st));
+        hipEvent_t e0, e1;
+        WM_CHECK(hipEventCreate(&e0));
+        WM_CHECK(hipEventCreate(&e1));
+        launch_attn_encoder(ctx->c.dt, qkv, out, B, T, d, H, st, variant);
+        WM_CHECK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; r++) launch_attn_encoder(ctx->c.dt, qkv, out, B, T, d, H, st, variant);
+        WM_CHECK(hipEventRecord(e1, st));
+        WM_CHECK(hipStreamSynchronize(st));
+        float t = 0;
+        WM_CHECK(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = reps > 0 ? t / reps : 0.0f;
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        hipStreamDestroy(st);
+        return 0;
+    });
+}
+
 int whisper_mi355x_debug_gemm_ln(struct whisper_context* ctx, const void* A, int M, int K, const void* B, int N,
                                  const float* bias, float* x, const float* ln_w, const float* ln_b, void* y, int reps,
                                  float* ms) {

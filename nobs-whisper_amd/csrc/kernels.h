@@ -121,7 +121,9 @@ void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------
 // encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)
-void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int d, int H, hipStream_t st);
+// variant: -1 = WHISPER_MI355X_ATTN (default 2), else 1 / 2 / 3 (attn_enc_kernel / _enc2_ / _enc3_)
+void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int d, int H, hipStream_t st,
+                         int variant = -1);
 // single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:
 // token i attends keys [0, n_kv[i]) of slot[i]; q [n][q_stride] at head h offset h*64; out [n][d]
 void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache, const int* slot, const int* n_kv,

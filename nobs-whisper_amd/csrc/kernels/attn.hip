@@ -320,6 +320,169 @@ __global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qk
 }
 
 // ------------------------------------------------------------------------------------------------
+// attn_enc2_kernel software-pipelined across key tiles (WHISPER_MI355X_ATTN=3): iteration t issues the
+// score MFMAs of tile t+1 first, then runs the softmax of tile t and its P.V MFMAs, so a wave has
+// independent MFMA work in flight under its exponentials instead of alternating MFMA-only and
+// VALU-only phases in lockstep with its SIMD partner. K runs one tile ahead of V in the same two LDS
+// slots each: iteration t reads K(t+1) and V(t) and fills K(t+2), V(t+1). Every per-element operation
+// and its order is attn_enc2_kernel's, so the outputs are bit-identical.
+template <typename T>
+__global__ void __launch_bounds__(512) attn_enc3_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
+    typedef typename Frag<T>::type FT;
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int hh = lane >> 5, ql = lane & 31;
+    const long base = (long)b * Tn;
+    const int ld = 3 * d;
+    __shared__ u32x4 Ks[2][64 * 8];
+    __shared__ u32x4 Vs[2][64 * 8];
+    const u32x4 zero = {0, 0, 0, 0};
+
+    const int q = qb * 256 + wave * 32 + ql;
+    FT qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const u32x4 v = q < Tn ? *(const u32x4*)(qkv + (base + q) * ld + h * 64 + s * 16 + hh * 8) : zero;
+        qf[s] = __builtin_bit_cast(FT, v);
+    }
+    const int skey = tid >> 3, sch = tid & 7;
+    const int k_slot = skey * 8 + (sch ^ ((skey >> 1) & 7));
+    const int v_slot = skey * 8 + (sch ^ (((skey >> 1) & 1) << 2));
+    auto load_k = [&](int kt) -> u32x4 {
+        const int kg = kt * 64 + skey;
+        return kg < Tn ? *(const u32x4*)(qkv + (base + kg) * ld + d + h * 64 + sch * 8) : zero;
+    };
+    auto load_v = [&](int kt) -> u32x4 {
+        const int kg = kt * 64 + skey;
+        return kg < Tn ? *(const u32x4*)(qkv + (base + kg) * ld + 2 * d + h * 64 + sch * 8) : zero;
+    };
+    const int tg = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+    int vbase[2];
+#pragma unroll
+    for (int db = 0; db < 2; db++) {
+        const int ch = db * 4 + tg * 2 + (tp >> 1);
+        vbase[db] = (4 * hh + tq) * 128 + 16 * (ch ^ (((tq >> 1) & 1) << 2)) + 8 * (tp & 1);
+    }
+    const int n_kt = (Tn + 63) / 64;
+    // S^T of tile kt from K slot ks, masked past Tn
+    auto scores = [&](int kt, int ks, f32x16* sacc) {
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) sacc[kb][r] = 0.0f;
+            const int key = kb * 32 + ql;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const FT kf = __builtin_bit_cast(FT, Ks[ks][key * 8 + ((s * 2 + hh) ^ ((key >> 1) & 7))]);
+                sacc[kb] = mfma32x32x16(kf, qf[s], sacc[kb]);
+            }
+        }
+        if (kt * 64 + 64 > Tn) {
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int key = kt * 64 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    if (key >= Tn) sacc[kb][r] = -INFINITY;
+                }
+        }
+    };
+
+    f32x16 oacc[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) oacc[i][r] = 0.0f;
+    float m_run = -INFINITY, l_run = 0.0f;
+    const float c = 0.125f * 1.44269504088896340736f;
+
+    // prologue: K(0), V(0) -> slot 0, K(1) -> K slot 1; S(0)
+    Ks[0][k_slot] = load_k(0);
+    Vs[0][v_slot] = load_v(0);
+    if (n_kt > 1) Ks[1][k_slot] = load_k(1);
+    __syncthreads();
+    f32x16 scur[2];
+    scores(0, 0, scur);
+    __syncthreads();  // every wave has read K slot 0 before iteration 0 refills it with K(2)
+    for (int t = 0; t < n_kt; t++) {
+        const int cur = t & 1;
+        const bool more1 = t + 1 < n_kt, more2 = t + 2 < n_kt;
+        u32x4 nk = zero, nv = zero;
+        if (more2) nk = load_k(t + 2);
+        if (more1) nv = load_v(t + 1);
+        f32x16 snext[2];
+        if (more1) scores(t + 1, cur ^ 1, snext);
+        // softmax of tile t (attn_enc2_kernel's operations, same order)
+        float mx = scur[0][0];
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) mx = fmaxf(mx, scur[kb][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run, mx * c);
+        const bool moved = __builtin_amdgcn_ballot_w64(m_new != m_run) != 0;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        const f2 c2 = {c, c}, nm2 = {-m_new, -m_new};
+        FT pf[4];
+        f2 ls2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+            for (int sp = 0; sp < 2; sp++)
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const f2 x = {scur[kb][sp * 8 + j], scur[kb][sp * 8 + j + 1]};
+                    const f2 e = __builtin_elementwise_fma(x, c2, nm2);
+                    const f2 p = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+                    ls2 += p;
+                    pf[kb * 2 + sp][j] = (T)p.x;
+                    pf[kb * 2 + sp][j + 1] = (T)p.y;
+                }
+        l_run = l_run * alpha + (ls2.x + ls2.y);
+        if (moved) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) oacc[i][r] *= alpha;
+        }
+        const char* vimg = (const char*)Vs[cur];
+#pragma unroll
+        for (int db = 0; db < 2; db++)
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int r0 = (s >> 1) * 32 + (s & 1) * 16;
+                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + vbase[db] + r0 * 128));
+                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t)(vimg + vbase[db] + (r0 + 8) * 128));
+                const FT vf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                oacc[db] = mfma32x32x16(vf, pf[s], oacc[db]);
+            }
+        if (more2) Ks[cur][k_slot] = nk;
+        if (more1) Vs[cur ^ 1][v_slot] = nv;
+        __syncthreads();
+        if (more1) {
+            scur[0] = snext[0];
+            scur[1] = snext[1];
+        }
+    }
+    if (q >= Tn) return;
+    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32));
+    T* orow = out + (base + q) * d + h * 64;
+#pragma unroll
+    for (int db = 0; db < 2; db++)
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) {
+            T v4[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v4[j] = (T)(oacc[db][rr * 4 + j] * inv);
+            *(uint2*)(orow + db * 32 + rr * 8 + 4 * hh) = *(const uint2*)v4;
+        }
+}
+
+// ------------------------------------------------------------------------------------------------
 // FQ: q is not read from a buffer but reduced from the cross-Q projection's split-K slabs
 // (DecSlabs; q = (T)((sum_z + bias) * scale), the EPI_STORE epilogue of that GEMM).
 template <typename T, bool FQ>
@@ -765,11 +928,19 @@ void launch_attn_prefill(DType dt, const void* q, int q_stride, const void* cach
                                                           (const int2*)tiles, L, layer, H, ctx, d, (bf16_t*)out);
 }
 
-void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st) {
-    static const int variant = [] {
+void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st,
+                         int variant_arg) {
+    static const int variant_env = [] {
         const char* e = getenv("WHISPER_MI355X_ATTN");
         return e ? atoi(e) : 2;
     }();
+    const int variant = variant_arg >= 0 ? variant_arg : variant_env;
+    if (variant == 3 && d == H * 64) {
+        dim3 grid(cdiv(Tn, 256), H, B);
+        if (dt == DType::F16) attn_enc3_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
+        else attn_enc3_kernel<bf16_t><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
+        return;
+    }
     if (variant == 2 && d == H * 64) {
         dim3 grid(cdiv(Tn, 256), H, B);
         if (dt == DType::F16) attn_enc2_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);

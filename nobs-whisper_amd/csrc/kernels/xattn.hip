@@ -203,7 +203,7 @@ template <typename T, int NW, int CT, int AUX>
 __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
                                                              const T* __restrict__ qx, int Tn, int splits, float thr,
                                                              float* __restrict__ opart, float* __restrict__ ml, int rev,
-                                                             int wt) {
+                                                             int wt, int keep) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
@@ -272,8 +272,14 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
 #pragma unroll
         for (int k = 0; k < CT; k++) {
             const int gr = min(row0 + prow[k], Tn - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]), (lds_ptr_t)(st + (wave + k * NW) * 64),
-                                             16, 0, AUX);
+            // keep: the first `keep` clips' E with the default policy (candidates to stay in the MALL
+            // from one decoder layer to the next), the rest with AUX
+            if (i < keep)
+                __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]),
+                                                 (lds_ptr_t)(st + (wave + k * NW) * 64), 16, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]),
+                                                 (lds_ptr_t)(st + (wave + k * NW) * 64), 16, 0, AUX);
         }
     };
 
@@ -585,11 +591,14 @@ static void launch_step_t(const void* enc, const int* slot, const void* qx, int 
     static const int aux = getenv("WHISPER_MI355X_XNT") ? atoi(getenv("WHISPER_MI355X_XNT")) : 2;
     // WHISPER_MI355X_XO_WT=1: write-through partial-O stores (A/B)
     static const int wt = getenv("WHISPER_MI355X_XO_WT") ? atoi(getenv("WHISPER_MI355X_XO_WT")) : 0;
+    // WHISPER_MI355X_XKEEP=k: the first k clips' E loads use the default cache policy (A/B of MALL residency
+    // across decoder layers: k clips of large-v3 E are 3.84 MB each against a 256 MB MALL)
+    static const int keep = getenv("WHISPER_MI355X_XKEEP") ? atoi(getenv("WHISPER_MI355X_XKEEP")) : 0;
 #define WM_XSTEP(NW_, CT_)                                                                                                \
     if (aux == 2)                                                                                                          \
-        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt); \
+        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt, keep); \
     else                                                                                                                   \
-        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt)
+        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt, keep)
     switch (d) {
         case 384: WM_XSTEP(4, 3); break;
         case 512: WM_XSTEP(8, 2); break;

@@ -199,3 +199,77 @@ def test_gemm_small_matches_numpy(wrs, ctx, M, N, K, epi, lna):
     bound = (2e-3 if lna else 1e-4) * (np.abs(A64) @ np.abs(B64).T) + 1e-5 + 1e-6 * np.abs(ref)
     err = np.abs(out - ref)
     assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
+
+
+def _to_bf16_bits(x):
+    """float32 -> bf16 bit patterns (round to nearest even), and their float32 values"""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r, (r.astype(np.uint32) << 16).view(np.float32)
+
+
+def _attn_run(wrs, ctx, qkv_dev, B, T, d, H, variant, reps=0):
+    L = wrs.lib()
+    L.whisper_mi355x_debug_attn_encoder.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                    C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_float)]
+    out = np.zeros((B * T, d), np.uint16)
+    po = _dev(wrs, ctx, out)
+    ms = C.c_float()
+    assert L.whisper_mi355x_debug_attn_encoder(ctx.ptr, C.c_void_p(qkv_dev), B, T, d, H, variant, C.c_void_p(po),
+                                               reps, C.byref(ms)) == 0
+    L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(po), out.nbytes, 2)
+    L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(po))
+    return out, ms.value
+
+
+@pytest.mark.parametrize("dtype,B,T,H", [("BF16", 2, 1500, 20), ("F16", 3, 1500, 6), ("BF16", 1, 100, 8),
+                                         ("F16", 2, 64, 4)])
+def test_attn_encoder_pipelined_equals_enc2(wrs, micro_model, dtype, B, T, H):
+    """attn_enc3_kernel (score MFMAs of the next key tile issued under the softmax of the current one)
+    == attn_enc2_kernel bit for bit (same per-element operations and order), and both against a float64
+    softmax(Q K^T / 8) V of the same rounded operands."""
+    c = wrs.WhisperContext(micro_model, dtype=getattr(wrs, dtype))
+    d = 64 * H
+    rng = np.random.default_rng(B * 1000 + T + H)
+    x = rng.standard_normal((B * T, 3 * d), dtype=np.float32) * 1.5
+    if dtype == "BF16":
+        bits, xv = _to_bf16_bits(x)
+    else:
+        h = x.astype(np.float16)
+        bits, xv = h.view(np.uint16), h.astype(np.float32)
+    L = wrs.lib()
+    p = _dev(wrs, c, np.ascontiguousarray(bits))
+    o2, _ = _attn_run(wrs, c, p, B, T, d, H, 2)
+    o3, _ = _attn_run(wrs, c, p, B, T, d, H, 3)
+    L.whisper_mi355x_dev_free(c.ptr, C.c_void_p(p))
+    c.close()
+    assert np.array_equal(o2, o3), int((o2 != o3).sum())
+    val = ((o2.astype(np.uint32) << 16).view(np.float32) if dtype == "BF16" else o2.view(np.float16).astype(np.float32))
+    q, k, v = (xv[:, :d].reshape(B, T, H, 64), xv[:, d:2 * d].reshape(B, T, H, 64), xv[:, 2 * d:].reshape(B, T, H, 64))
+    for bb in range(B):
+        for hh in range(0, H, max(1, H // 3)):
+            s = q[bb, :, hh].astype(np.float64) @ k[bb, :, hh].astype(np.float64).T / 8.0
+            pm = np.exp(s - s.max(1, keepdims=True))
+            ref = (pm / pm.sum(1, keepdims=True)) @ v[bb, :, hh].astype(np.float64)
+            got = val.reshape(B, T, H, 64)[bb, :, hh]
+            tol = (2e-2 if dtype == "BF16" else 4e-3) * np.abs(v[bb, :, hh]).max()
+            assert np.abs(got - ref).max() <= tol, (bb, hh, np.abs(got - ref).max(), tol)
+
+
+def test_attn_encoder_variant_timing(wrs, micro_model):
+    """large-v3 shape, one 32-window launch (the engine's encoder group): time attn_enc2 vs attn_enc3."""
+    c = wrs.WhisperContext(micro_model, dtype=wrs.BF16)
+    B, T, H = 32, 1500, 20
+    d = 64 * H
+    rng = np.random.default_rng(5)
+    bits, _ = _to_bf16_bits(rng.standard_normal((B * T, 3 * d), dtype=np.float32))
+    L = wrs.lib()
+    p = _dev(wrs, c, bits)
+    o2, ms2 = _attn_run(wrs, c, p, B, T, d, H, 2, reps=5)
+    o3, ms3 = _attn_run(wrs, c, p, B, T, d, H, 3, reps=5)
+    L.whisper_mi355x_dev_free(c.ptr, C.c_void_p(p))
+    c.close()
+    flop = 4.0 * B * H * T * T * 64
+    print(f"attn_enc2 {ms2 * 1e3:.1f} us ({flop / ms2 / 1e9:.0f} TF/s), attn_enc3 {ms3 * 1e3:.1f} us "
+          f"({flop / ms3 / 1e9:.0f} TF/s)")
+    assert np.array_equal(o2, o3)
