@@ -62,7 +62,14 @@ def ensure_model(path: str, shape: str):
     from make_model import write_model
     if not os.path.exists(path):
         t = time.time()
-        write_model(path, shape, 0)
+        last = [t]
+
+        def progress(name):  # a quantized large-v3 takes minutes to write: say that it moves
+            if time.time() - last[0] > 20:
+                last[0] = time.time()
+                log(f"[bench] writing {shape}: {name} ({time.time() - t:.0f}s)")
+
+        write_model(path, shape, 0, progress=progress)
         log(f"[bench] wrote synthetic {shape} model to {path} in {time.time() - t:.1f}s")
 
 
@@ -370,6 +377,9 @@ def main():
                     help="also time the app's per-call pattern (fresh state per 25 s chunk, whisper.rs:66-148) "
                          "on base f16 and this model in its dtype (rank 0)")
     ap.add_argument("--app-calls", type=int, default=6)
+    ap.add_argument("--quant", default="none", choices=["none", "q4_0", "q4_1", "q5_0", "q5_1", "q8_0"],
+                    help="GGML block-quantized model file (the app's catalog ships large-v3-q5_0): blocks stay "
+                         "quantized in HBM, dequantized inside the GEMMs")
     ap.add_argument("--weights", default="conf", choices=["conf", "plain"],
                     help="synthetic weight init: conf = a decoder as peaked as a trained one (tools/make_model.py "
                          "+conf), so real greedy termination happens; plain = i.i.d. random")
@@ -403,7 +413,7 @@ def main():
 
     wrs = load_wrs()
     os.makedirs(args.model_dir, exist_ok=True)
-    shape = args.model + ("+conf" if args.weights == "conf" else "")
+    shape = args.model + ("+conf" if args.weights == "conf" else "") + ("" if args.quant == "none" else "+" + args.quant)
     model_path = os.path.join(args.model_dir, f"{shape}_s0.bin")
     if local_rank == 0:
         ensure_model(model_path, shape)
@@ -578,6 +588,10 @@ def main():
                            frac=round(pw["dec_bytes_per_step"] * (args.tokens - 1) / max(1e-9, dec_s) / 1e9 / HBM_PEAK_GBS, 4),
                            bytes_split_gb={k: round(pw[k] / 1e9, 3) for k in ("dec_weight_bytes", "dec_cross_bytes", "dec_self_bytes")}),
         }
+        if args.quant != "none":  # phase_work prices the decoder weights at 2 B each
+            roof["phases"]["decode"]["note"] = f"{args.quant} file: bytes priced as 16-bit weights (the blocks stream fewer)"
+        pa, pn = C.c_void_p(), C.c_size_t()
+        arena_bytes = pn.value if wrs.lib().whisper_mi355x_weight_arena(ctx.ptr, C.byref(pa), C.byref(pn)) == 0 else None
         app = None
         if args.app_pattern:
             app = []
@@ -602,10 +616,12 @@ def main():
             "data": ("synthetic (seeded AM-harmonic 30 s PCM; seeded random weights of the named architecture"
                      + (", decoder init as peaked as a trained model's: tools/make_model.py +conf)" if args.weights == "conf"
                         else ")")),
-            "config": {"workload": f"{args.model} {args.dtype} greedy, {global_batch} x 30 s chunks per step over "
+            "config": {"workload": f"{args.model}{'' if args.quant == 'none' else '-' + args.quant} {args.dtype} greedy, "
+                                   f"{global_batch} x 30 s chunks per step over "
                                    f"{world} GPU(s) ({nb} on rank 0), fixed {args.tokens}-token decode per chunk, "
                                    f"language en, no prompt",
-                       "model": args.model, "global_batch": global_batch, "batch_per_gpu": nb,
+                       "model": args.model, "quant": None if args.quant == "none" else args.quant,
+                       "global_batch": global_batch, "batch_per_gpu": nb,
                        "tokens_per_chunk": args.tokens, "seq_len": 1500,
                        "parallelism": f"dp{world} (chunk sharding, RCCL weight broadcast only)"},
             "roofline": roof,
@@ -616,7 +632,8 @@ def main():
                       "cross_form": "direct" if form["direct"] else "cache",
                       "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
                       "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),
-                      "weight_broadcast_s": round(bcast_s, 3), "frontend": frontend},
+                      "weight_broadcast_s": round(bcast_s, 3), "frontend": frontend,
+                      "weight_arena_bytes": arena_bytes},
         }
         print(json.dumps(line), flush=True)
     L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(buf))

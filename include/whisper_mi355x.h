@@ -138,8 +138,8 @@ WHISPER_API int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context * ctx, i
 WHISPER_API int whisper_mi355x_debug_quant_fp8(struct whisper_context * ctx, const void * x, long rows, int K,
                                                void * q, float * s);
 /* Debug/tuning: one encoder self-attention launch (device pointers): qkv [B*T][3d] (Q | K | V, compute
- * type of ctx), out [B*T][d]; variant 1 / 2 / 3 = attn_enc_kernel / attn_enc2_kernel / attn_enc3_kernel
- * (d = 64 H). The first launch's result stays in out; reps more launches are timed (ms per launch). */
+ * type of ctx), out [B*T][d]; variant 1 / 2 / 3 / 5 = attn_enc_kernel / attn_enc2_kernel / attn_enc3_kernel /
+ * attn_enc2_kernel held to 128 VGPRs, two workgroups per CU (d = 64 H). The first launch's result stays in out; reps more launches are timed (ms per launch). */
 WHISPER_API int whisper_mi355x_debug_attn_encoder(struct whisper_context * ctx, const void * qkv, int B, int T, int d,
                                                   int H, int variant, void * out, int reps, float * ms);
 WHISPER_API int whisper_mi355x_debug_gemm_ln(struct whisper_context * ctx, const void * A, int M, int K,

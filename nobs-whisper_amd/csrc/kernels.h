@@ -42,7 +42,7 @@ enum Epi : int {
     EPI_F32 = 4,       // f32 out = v                                       (logits)
     EPI_CROSSKV = 5,   // T scatter into cross cache [slot][L][2][H][ctx][64]; K columns scaled
     EPI_QKV_DEC = 6,   // n<d: T q[m][n]*scale ; d<=n<2d: K cache (scaled) ; 2d<=n<3d: V cache
-    EPI_GELU_F = 7,    // T out = tanh-GELU by formula in f32 (fp8 mode only: not ggml's f16 table)
+    EPI_GELU_F = 7,    // T out = tanh-GELU by formula in f32 (fp8 mode, and bf16 encoders: not ggml's f16 table)
     EPI_GELU_MX = 8,   // fp8 mode: GELU by formula, then MX e4m3: out bytes [M][N] = e4m3(v / 2^e) with one
                        // power-of-two scale per row and 32-column block, mx_scale[m][n/32] = e + 127 (E8M0)
 };
@@ -121,7 +121,8 @@ void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------
 // encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)
-// variant: -1 = WHISPER_MI355X_ATTN (default 2), else 1 / 2 / 3 (attn_enc_kernel / _enc2_ / _enc3_)
+// variant: -1 = WHISPER_MI355X_ATTN (default 5), else 1 / 2 / 3 / 5 (attn_enc_kernel / _enc2_ / _enc3_ /
+// _enc2_ held to 128 VGPRs)
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int d, int H, hipStream_t st,
                          int variant = -1);
 // single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:

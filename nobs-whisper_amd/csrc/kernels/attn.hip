@@ -163,8 +163,12 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(const T* __restrict__ qkv
 //                             the permuted key order of that layout), A = V^T via
 //                             ds_read_b64_tr_b16 from a row-major V image (no transposing store)
 // Exponentials in base 2 with the 1/8 scale and log2(e) folded into one FMA.
-template <typename T>
-__global__ void __launch_bounds__(512) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
+// MINW = 4 (variant 5, the default): the register allocation held to 128 VGPRs so that two workgroups
+// share a CU (4 waves per SIMD); they drift apart between their barriers, so one workgroup's softmax
+// runs beside the other's MFMAs: 578 vs 694 us per 32-window large-v3 launch (random bf16 operands,
+// profiles/r03_attn_encoder_variants.txt). MINW = 1 (variant 2): 138 VGPRs, one workgroup per CU.
+template <typename T, int MINW = 1>
+__global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
     typedef typename Frag<T>::type FT;
     typedef short v4s __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
@@ -932,13 +936,19 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
                          int variant_arg) {
     static const int variant_env = [] {
         const char* e = getenv("WHISPER_MI355X_ATTN");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : 5;
     }();
     const int variant = variant_arg >= 0 ? variant_arg : variant_env;
     if (variant == 3 && d == H * 64) {
         dim3 grid(cdiv(Tn, 256), H, B);
         if (dt == DType::F16) attn_enc3_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
         else attn_enc3_kernel<bf16_t><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
+        return;
+    }
+    if (variant == 5 && d == H * 64) {
+        dim3 grid(cdiv(Tn, 256), H, B);
+        if (dt == DType::F16) attn_enc2_kernel<half_t, 4><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
+        else attn_enc2_kernel<bf16_t, 4><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
         return;
     }
     if (variant == 2 && d == H * 64) {

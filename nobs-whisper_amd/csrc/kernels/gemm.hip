@@ -86,11 +86,13 @@ __device__ __forceinline__ void gelu_ltab_stage(char* dst, int tid) {
     }
 }
 
-// tanh-GELU by formula, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)), for the fp8 mode (which is not
-// a whisper.cpp-parity path, so it skips the table and its 75.8 KB LDS copy per tile)
+// tanh-GELU by formula, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)), for the fp8 mode and bf16
+// encoders (neither is a bit-exact whisper.cpp path, so they skip the table and its 75.8 KB LDS copy
+// per tile). The quotient is x * rcp(1 + e) (v_rcp_f32, ~1 ulp of f32) instead of IEEE division's
+// scale / fma / fixup sequence: the result is rounded to bf16 (2^-9) right after.
 __device__ __forceinline__ float gelu_formula(float x) {
     const float u = 1.5957691216057308f * (x + 0.044715f * x * x * x);
-    return x / (1.0f + __expf(-u));
+    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-u));
 }
 
 template <int EPI, typename T>

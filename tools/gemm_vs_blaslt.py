@@ -18,7 +18,7 @@ d = 1280
 B_WIN = int(os.environ.get("B_WIN", "32"))
 for (M, N, K, name, epi) in [(B_WIN * 1500, 3 * d, d, "qkv", 0), (B_WIN * 1500, d, d, "out", 2),
                              (B_WIN * 1500, 4 * d, d, "fc1", 1), (B_WIN * 1500, d, 4 * d, "fc2", 2),
-                             (B_WIN * 1500, 4 * d, d, "fc1-store", 0)]:
+                             (B_WIN * 1500, 4 * d, d, "fc1-gelu_f", 7), (B_WIN * 1500, 4 * d, d, "fc1-store", 0)]:
     A = rng.standard_normal((M, K)).astype(np.float16)
     B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
     bias = np.zeros(N, np.float32)
@@ -40,5 +40,31 @@ for (M, N, K, name, epi) in [(B_WIN * 1500, 3 * d, d, "qkv", 0), (B_WIN * 1500, 
     torch.cuda.synchronize()
     tms = e0.elapsed_time(e1) / 10
     f = 2.0 * M * N * K
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 10
+
+    # the same epilogue through hipBLASLt where torch exposes it: f32 residual C = D (beta = 1) for epi 2,
+    # the bias + GELU epilogue for epi 1
+    fair = ""
+    try:
+        if epi == 2:
+            resid = torch.zeros((M, N), dtype=torch.float32, device="cuda")
+            t2 = timed(lambda: torch.addmm(resid, ta, tb.t(), out_dtype=torch.float32))
+            fair = f" | hipBLASLt f32 C+=AB {t2:.3f} ms {f / t2 / 1e9:.0f} TF/s"
+        elif epi in (1, 7):
+            bb = torch.zeros(N, dtype=torch.bfloat16, device="cuda")
+            t2 = timed(lambda: torch._addmm_activation(bb, ta, tb.t(), use_gelu=True))
+            fair = f" | hipBLASLt bias+GELU {t2:.3f} ms {f / t2 / 1e9:.0f} TF/s"
+    except Exception as ex:  # noqa: BLE001
+        fair = f" | fair variant unavailable: {type(ex).__name__}: {str(ex)[:80]}"
     print(f"{name:9s} M={M} N={N} K={K}: engine epi{epi} [{', '.join(res)}] TF/s | hipBLASLt {tms:.3f} ms "
-          f"{f / tms / 1e9:.0f} TF/s", flush=True)
+          f"{f / tms / 1e9:.0f} TF/s{fair}", flush=True)

@@ -349,10 +349,12 @@ def dequantize_rows(raw: bytes, qtype: str, n: int) -> np.ndarray:
     return y.reshape(-1)[:n]
 
 
-def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, qtype: str | None = None) -> dict:
+def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, qtype: str | None = None,
+                progress=None) -> dict:
     """Write a seeded synthetic model. Returns the hparams dict. ftype 1 = f16 matrices, 0 = all f32.
     shape may carry the "+conf" suffix (see CONF_SCALE) and a "+q5_0" / "+q5_1" / "+q8_0" / "+q4_0" /
-    "+q4_1" suffix: every 2-D tensor but QUANT_SKIP quantized as whisper.cpp's quantize tool does."""
+    "+q4_1" suffix: every 2-D tensor but QUANT_SKIP quantized as whisper.cpp's quantize tool does.
+    progress(name), if given, is called before every tensor (long writes can report that they move)."""
     for q in GGML_TYPES:
         if shape.endswith("+" + q):
             shape, qtype = shape[:-len(q) - 1], q
@@ -376,6 +378,8 @@ def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, q
             f.write(struct.pack("<I", len(t)))
             f.write(t)
         for name, shp, is_f32 in tensor_specs(n_vocab, n_mels, d, n_enc, n_dec):
+            if progress is not None:
+                progress(name)
             data = init_tensor(rng, name, shp, d, n_mels)
             if conf:
                 data = conf_adjust(name, data, n_vocab)
