@@ -188,6 +188,7 @@ void whisper_free(struct whisper_context* ctx) {
     if (ctx->c.default_state) free_state(ctx->c.default_state);
     ctx->c.default_state = nullptr;
     drain_state_pool(&ctx->c);
+    orphan_states(&ctx->c);  // states the caller still holds stay valid to whisper_free_state
     free_context(&ctx->c);  // weight arena + the fp8 arena
     delete ctx;
 }

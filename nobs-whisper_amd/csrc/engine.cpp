@@ -148,6 +148,7 @@ static whisper_state* create_state(Context* c) {
     WM_CHECK(hipSetDevice(c->device));
     whisper_state* s = new whisper_state();
     s->ctx = c;
+    s->device = c->device;
     try {
         WM_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         WM_CHECK(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
@@ -161,6 +162,8 @@ static whisper_state* create_state(Context* c) {
         delete s;
         throw;
     }
+    std::lock_guard<std::mutex> lk(c->pool_mu);
+    c->live.push_back(s);
     return s;
 }
 
@@ -212,7 +215,11 @@ whisper_state* new_state(Context* c) {
 static void free_ws(Workspace& w);
 
 static void destroy_state(whisper_state* s) {
-    hipSetDevice(s->ctx->device);
+    if (Context* c = s->ctx) {
+        std::lock_guard<std::mutex> lk(c->pool_mu);
+        c->live.erase(std::remove(c->live.begin(), c->live.end(), s), c->live.end());
+    }
+    hipSetDevice(s->device);
     hipStreamSynchronize(s->stream);
     hipStreamSynchronize(s->stream2);
     drop_graphs(s);
@@ -229,6 +236,10 @@ static void destroy_state(whisper_state* s) {
 void free_state(whisper_state* s) {
     if (!s) return;
     Context* c = s->ctx;
+    if (!c) {  // its context is gone: nothing to pool into
+        destroy_state(s);
+        return;
+    }
     hipSetDevice(c->device);
     const bool healthy = hipStreamSynchronize(s->stream) == hipSuccess && hipStreamSynchronize(s->stream2) == hipSuccess &&
                          s->kpending.empty();
@@ -251,9 +262,15 @@ void drain_state_pool(Context* c) {
     for (whisper_state* s : p) destroy_state(s);
 }
 
+void orphan_states(Context* c) {
+    std::lock_guard<std::mutex> lk(c->pool_mu);
+    for (whisper_state* s : c->live) s->ctx = nullptr;
+    c->live.clear();
+}
+
 void recover_state(whisper_state* s) {
     if (!s) return;
-    hipSetDevice(s->ctx->device);
+    hipSetDevice(s->device);
     for (hipStream_t st : {s->stream, s->stream2}) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
@@ -967,8 +984,18 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
         return;
     }
+    // WHISPER_MI355X_DBG_SAMEW=1 (timing experiment only, results are wrong): every decoder layer reads
+    // layer 0's weights, so they stay L2/MALL-hot across the step (upper bound of a weight prefetch).
+    // Measured: decode 856 -> 846 ms per step at 128 clips, 406 -> 403 at 16: the chain is not waiting
+    // for HBM (profiles/r03_envab_decode_cache.txt; a side-branch prefetch of the next layer's weights
+    // made it slower, 1066-1081 ms)
+    static const bool samew = [] {
+        const char* e = getenv("WHISPER_MI355X_DBG_SAMEW");
+        return e && atoi(e) == 1;
+    }();
     for (int l = 0; l < L; l++) {
-        LayerW Lw = W.dec[l];
+        const int lw = samew && fused ? 0 : l;
+        LayerW Lw = W.dec[lw];
         if (c->quant) {  // prefill / language detection: this layer's blocks dequantized into the scratch
             const LayerMats m = layer_mats(c, s, Lw, st);
             Lw.wqkv = (void*)m.wqkv; Lw.wo = (void*)m.wo; Lw.wxq = (void*)m.wxq; Lw.wxo = (void*)m.wxo;
@@ -995,7 +1022,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
             // -> one pass over E per clip -> split merge + Wv. Decode steps: the cross-Q GEMM leaves
             // split-K slabs that the Q' projection reduces itself (one launch fewer per layer)
-            const void* wkt_l = (const char*)W.wkT + (size_t)l * H * d * 64 * 2;
+            const void* wkt_l = (const char*)W.wkT + (size_t)lw * H * d * 64 * 2;
             if (fused && xq_fused()) {
                 const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);
                 KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * d * sl.splits + 4.0 * n_tok * H * d, st);
@@ -1015,8 +1042,8 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             }
             {
                 KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d, st);
-                launch_xattn_combine(dt, v.xo, v.xml, S, (const char*)W.wkv_cross + (size_t)(2 * l + 1) * d * d * 2,
-                                     W.bkv_cross + (size_t)(2 * l + 1) * d, n_tok, d, H, datt, st);
+                launch_xattn_combine(dt, v.xo, v.xml, S, (const char*)W.wkv_cross + (size_t)(2 * lw + 1) * d * d * 2,
+                                     W.bkv_cross + (size_t)(2 * lw + 1) * d, n_tok, d, H, datt, st);
             }
         } else if (fused) {
             const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);

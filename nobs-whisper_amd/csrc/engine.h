@@ -109,6 +109,10 @@ struct Context {
     // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.
     std::mutex pool_mu;
     std::vector<whisper_state*> pool;
+    // every state of this context that is alive (pooled or held by a caller), under pool_mu:
+    // whisper_free orphans the ones a caller still holds, so a later whisper_free_state does not touch
+    // the freed context (a garbage collector may finalise a context before its states)
+    std::vector<whisper_state*> live;
 };
 
 struct TokenData {
@@ -179,7 +183,8 @@ struct KStat { double ms = 0, work = 0; long count = 0; };
 }  // namespace wm
 
 struct whisper_state {
-    wm::Context* ctx = nullptr;
+    wm::Context* ctx = nullptr;  // nullptr once the context was freed before the state (orphan)
+    int device = 0;
     hipStream_t stream = nullptr;
     // second stream + fork/join events: decode steps run their rows as two groups concurrently
     hipStream_t stream2 = nullptr;
@@ -230,6 +235,7 @@ void free_state(whisper_state* s);
 void recover_state(whisper_state* s);
 // frees the states kept in the context's pool (whisper_free)
 void drain_state_pool(Context* c);
+void orphan_states(Context* c);
 
 struct FullOpts {
     int fixed_tokens = 0;

@@ -659,6 +659,24 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     const long s = slot[i];
     T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
     T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
+    // Cached rows come in chunks of 64 (U = 8 rows per lane group). The first chunk of K and of V does not
+    // depend on this step's projection, so its loads are issued before the slab reduce and land under it
+    // (one memory round trip for the prologue, the first 64 scores and the first 64 P.V terms). Every
+    // per-key sum and the P.V order (t = grp, grp + 8, ... per lane group) are those of the
+    // 32-row-chunk loop this replaces.
+    constexpr int U = 8, CHR = 8 * U;
+    const u32x4 zero = {0, 0, 0, 0};
+    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const u32x4* src = (const u32x4*)(base + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+        }
+    };
+    u32x4 kr[U], vr[U];
+    load_rows(K, grp, kr);
+    load_rows(V, grp, vr);
     {
         const float* p = sl.ws + (long)i * sl.ld + h * 64 + lane;
         float vq = 0.0f, vk = 0.0f, vv = 0.0f;
@@ -684,17 +702,8 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
-    constexpr int U = 4;
-    const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
-    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 8 * u;
-            const u32x4* src = (const u32x4*)(K + (long)t * 64 + lane8 * 8);
-            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
-        }
+    auto scores = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
@@ -708,6 +717,12 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
                 lmax = fmaxf(lmax, a);
             }
         }
+    };
+    scores(grp, kr);
+    for (int t0 = grp + CHR; t0 < pos; t0 += CHR) {
+        u32x4 raw[U];
+        load_rows(K, t0, raw);
+        scores(t0, raw);
     }
     {  // the fresh key (position pos)
         float a = 0.0f;
@@ -733,14 +748,7 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 8 * u;
-            const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
-            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
-        }
+    auto pv = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
@@ -749,6 +757,12 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
         }
+    };
+    pv(grp, vr);
+    for (int t0 = grp + CHR; t0 < pos; t0 += CHR) {
+        u32x4 raw[U];
+        load_rows(V, t0, raw);
+        pv(t0, raw);
     }
     if (grp == 0) {
         const float p = sc[w][pos];

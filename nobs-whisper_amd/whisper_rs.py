@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 from dataclasses import dataclass
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -219,6 +220,7 @@ class WhisperContext:
         cp.gpu_device = gpu_device
         self.L = L
         self.gpu_device = gpu_device
+        self._states = weakref.WeakSet()
         self.ptr = L.whisper_mi355x_init(path.encode(), cp, dtype, load_weights)
         if not self.ptr:
             raise RuntimeError(f"whisper_mi355x_init failed for {path}")
@@ -232,6 +234,7 @@ class WhisperContext:
         cp.use_gpu = use_gpu
         self.L = L
         self.gpu_device = cp.gpu_device
+        self._states = weakref.WeakSet()
         self.ptr = L.whisper_init_from_file_with_params_no_state(path.encode(), cp)
         if not self.ptr:
             raise RuntimeError(f"failed to load {path}")
@@ -246,6 +249,10 @@ class WhisperContext:
         return list(buf[:n])
 
     def close(self):
+        # states first, as whisper.h requires (a garbage collector may finalise a context and its
+        # states in any order; the library also tolerates the reverse order)
+        for st in list(getattr(self, "_states", ())):
+            st.close()
         if self.ptr:
             self.L.whisper_free(self.ptr)
             self.ptr = None
@@ -264,6 +271,7 @@ class WhisperState:
         self.ptr = self.L.whisper_init_state(ctx.ptr)
         if not self.ptr:
             raise RuntimeError("whisper_init_state failed")
+        ctx._states.add(self)
 
     def full(self, params: FullParams, audio) -> int:
         import numpy as np

@@ -126,3 +126,27 @@ def test_recycled_state_equals_fresh_state(wrs, monkeypatch, shape, dtype):
             assert st.info()["graphs"] >= 1
         st.close()
     ctx.close()
+
+
+def test_state_outliving_its_context(wrs):
+    """A garbage collector may finalise a context before its states (the round-3 suite crashed at
+    interpreter exit that way): whisper_free orphans the states a caller still holds, and a later
+    whisper_free_state releases them without touching the freed context. The Python wrapper also
+    closes a context's states first."""
+    from conftest import model_path
+    path = model_path("tiny.en")
+    ctx = wrs.WhisperContext(path)
+    L = ctx.L
+    a, b = ctx.create_state(), ctx.create_state()
+    assert a.full(wrs.reference_full_params("en"), synthetic_pcm(0)) == 0
+    b.close()  # pooled: whisper_free destroys it with the pool
+    raw = a.ptr
+    a.ptr = None  # the wrapper no longer owns it: free it by hand after the context
+    L.whisper_free(ctx.ptr)
+    ctx.ptr = None
+    L.whisper_free_state(raw)  # orphan: must not touch the freed context
+    # wrapper order: closing the context closes its live states first
+    ctx2 = wrs.WhisperContext(path)
+    st = ctx2.create_state()
+    ctx2.close()
+    assert st.ptr is None
