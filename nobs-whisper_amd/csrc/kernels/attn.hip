@@ -504,6 +504,23 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     __shared__ float red[256];
     __shared__ float acc_s[32][65];
 
+    // Loads: U key rows per lane group per chunk, the next chunk issued before the current one is
+    // consumed (two chunks in flight); the first K chunk is issued before q is formed (it does not
+    // depend on q) and the first V chunk before the softmax (it does not depend on P). The arithmetic
+    // (per-key sums, the block max, the sum tree, P rounded to T, the P.V order per lane group) is
+    // the round-2 kernel's: the sum keeps its tree association (lanes t, t+64, t+128, t+192 first,
+    // then halving inside one wave), with 2 barriers instead of 9.
+    constexpr int U = 8, CHR = 32 * U;
+    const u32x4 zero = {0, 0, 0, 0};
+    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 32 * u;
+            raw[u] = t < n_kv ? *(const u32x4*)(base + (long)t * 64 + lane8 * 8) : zero;
+        }
+    };
+    u32x4 ra[U], rb[U];
+    load_rows(K, grp, ra);
     float qv[8];
     if constexpr (FQ) {
         if (tid < 64) {
@@ -523,18 +540,9 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
 #pragma unroll
         for (int e = 0; e < 8; e++) qv[e] = (float)qe[e];
     }
-    // phase 1: scores; U key rows in flight per lane group before the first use (U = 16 measured no
-    // faster at 16 clips)
-    constexpr int U = 8;
-    const u32x4 zero = {0, 0, 0, 0};
+    // phase 1: scores
     float lmax = -INFINITY;
-    for (int t0 = grp; t0 < n_kv; t0 += 32 * U) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 32 * u;
-            raw[u] = t < n_kv ? *(const u32x4*)(K + (long)t * 64 + lane8 * 8) : zero;
-        }
+    auto scores = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 32 * u;
@@ -550,28 +558,39 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
                 lmax = fmaxf(lmax, a);
             }
         }
+    };
+    {
+        int t0 = grp;
+        for (; t0 + CHR < n_kv; t0 += 2 * CHR) {
+            load_rows(K, t0 + CHR, rb);
+            scores(t0, ra);
+            if (t0 + 2 * CHR < n_kv) load_rows(K, t0 + 2 * CHR, ra);
+            scores(t0 + CHR, rb);
+        }
+        if (t0 < n_kv) scores(t0, ra);
     }
-    // block max
-    red[tid] = lmax;
+    load_rows(V, grp, ra);  // lands under the softmax
+    // block max (order-free), then the sum in the round-2 tree's association
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) red[wave] = lmax;
     __syncthreads();
-    for (int o2 = 128; o2 > 0; o2 >>= 1) {
-        if (tid < o2) red[tid] = fmaxf(red[tid], red[tid + o2]);
-        __syncthreads();
-    }
-    const float mx = red[0];
-    __syncthreads();
+    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     float lsum = 0.0f;
     for (int t = tid; t < n_kv; t += 256) {
         const float e = expf(sc[t] - mx);
         sc[t] = e;
         lsum += e;
     }
+    __syncthreads();  // every wave has read red[0..3]
     red[tid] = lsum;
     __syncthreads();
-    for (int o2 = 128; o2 > 0; o2 >>= 1) {
-        if (tid < o2) red[tid] += red[tid + o2];
-        __syncthreads();
+    if (wave == 0) {
+        float r = (red[lane] + red[lane + 128]) + (red[lane + 64] + red[lane + 192]);
+        for (int o = 32; o > 0; o >>= 1) r = r + __shfl_down(r, o);
+        if (lane == 0) red[0] = r;
     }
+    __syncthreads();
     const float inv = 1.0f / red[0];
     for (int t = tid; t < n_kv; t += 256) sc[t] = (float)(T)(sc[t] * inv);  // P rounded as ggml's f16 src1
     __syncthreads();
@@ -579,13 +598,7 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    for (int t0 = grp; t0 < n_kv; t0 += 32 * U) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 32 * u;
-            raw[u] = t < n_kv ? *(const u32x4*)(V + (long)t * 64 + lane8 * 8) : zero;
-        }
+    auto pv = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 32 * u;
@@ -594,6 +607,16 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
         }
+    };
+    {
+        int t0 = grp;
+        for (; t0 + CHR < n_kv; t0 += 2 * CHR) {
+            load_rows(V, t0 + CHR, rb);
+            pv(t0, ra);
+            if (t0 + 2 * CHR < n_kv) load_rows(V, t0 + 2 * CHR, ra);
+            pv(t0 + CHR, rb);
+        }
+        if (t0 < n_kv) pv(t0, ra);
     }
 #pragma unroll
     for (int e = 0; e < 8; e++) acc_s[grp][lane8 * 8 + e] = acc[e];
@@ -659,24 +682,6 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     const long s = slot[i];
     T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
     T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
-    // Cached rows come in chunks of 64 (U = 8 rows per lane group). The first chunk of K and of V does not
-    // depend on this step's projection, so its loads are issued before the slab reduce and land under it
-    // (one memory round trip for the prologue, the first 64 scores and the first 64 P.V terms). Every
-    // per-key sum and the P.V order (t = grp, grp + 8, ... per lane group) are those of the
-    // 32-row-chunk loop this replaces.
-    constexpr int U = 8, CHR = 8 * U;
-    const u32x4 zero = {0, 0, 0, 0};
-    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 8 * u;
-            const u32x4* src = (const u32x4*)(base + (long)t * 64 + lane8 * 8);
-            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
-        }
-    };
-    u32x4 kr[U], vr[U];
-    load_rows(K, grp, kr);
-    load_rows(V, grp, vr);
     {
         const float* p = sl.ws + (long)i * sl.ld + h * 64 + lane;
         float vq = 0.0f, vk = 0.0f, vv = 0.0f;
@@ -702,8 +707,17 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
+    constexpr int U = 4;
+    const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
-    auto scores = [&](int t0, const u32x4 (&raw)[U]) {
+    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const u32x4* src = (const u32x4*)(K + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
@@ -717,12 +731,6 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
                 lmax = fmaxf(lmax, a);
             }
         }
-    };
-    scores(grp, kr);
-    for (int t0 = grp + CHR; t0 < pos; t0 += CHR) {
-        u32x4 raw[U];
-        load_rows(K, t0, raw);
-        scores(t0, raw);
     }
     {  // the fresh key (position pos)
         float a = 0.0f;
@@ -748,7 +756,14 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    auto pv = [&](int t0, const u32x4 (&raw)[U]) {
+    for (int t0 = grp; t0 < pos; t0 += 8 * U) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
@@ -757,12 +772,6 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
         }
-    };
-    pv(grp, vr);
-    for (int t0 = grp + CHR; t0 < pos; t0 += CHR) {
-        u32x4 raw[U];
-        load_rows(V, t0, raw);
-        pv(t0, raw);
     }
     if (grp == 0) {
         const float p = sc[w][pos];
