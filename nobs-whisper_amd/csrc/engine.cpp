@@ -628,9 +628,14 @@ static LayerMats layer_mats(Context* c, whisper_state* s, const LayerW& L, hipSt
     const int d = c->hp.n_audio_state;
     const size_t E = esize(c->dt);
     char* p = (char*)s->ws.wdq;
+    // one launch for the layer when its blocks share one type (a ggml file quantizes every projection
+    // alike), else one per matrix
+    DequantJobs J;
+    bool one_type = true;
     auto one = [&](const QMat& q, long rows, int K, const void*& dst) {
         if (!q.type) return;
-        launch_dequant(c->dt, q, rows, K, p, st);
+        if (J.n && q.type != J.q[0].type) one_type = false;
+        J.q[J.n] = q; J.rows[J.n] = rows; J.K[J.n] = K; J.out[J.n] = p; J.n++;
         dst = p;
         p += (size_t)rows * K * E;
     };
@@ -640,6 +645,9 @@ static LayerMats layer_mats(Context* c, whisper_state* s, const LayerW& L, hipSt
     one(L.qxo, d, d, m.wxo);
     one(L.q1, 4L * d, d, m.w1);
     one(L.q2, d, 4 * d, m.w2);
+    if (one_type) launch_dequant_multi(c->dt, J, st);
+    else
+        for (int j = 0; j < J.n; j++) launch_dequant(c->dt, J.q[j], J.rows[j], J.K[j], J.out[j], st);
     return m;
 }
 
@@ -819,6 +827,15 @@ static bool small_m_steps() {
     return on;
 }
 
+// Decode steps of block-quantized files: up to this many clips the small-M path reads the blocks
+// in its GEMMs; above it (its 32-row chunks each re-read the blocks: large-v3-q5_0 at 128 clips decoded
+// in 2534 ms per step against 857 for f16) the layer's blocks are dequantized once per step into the
+// scratch (one launch) and the split-K path runs as for f16 / bf16 weights. WHISPER_MI355X_QSMALL_MAX.
+static int quant_small_max() {
+    const char* e = getenv("WHISPER_MI355X_QSMALL_MAX");  // read per call (tests switch it)
+    return e ? atoi(e) : 32;
+}
+
 // Decode step over <= 32 rows (the app's one clip per call, whisper.rs:83-85 / state.rs:147; one
 // rank's 16-clip shard of configs[3] at 8 GPUs), kernels only: every projection is ONE launch of
 // gemm_small_kernel (no split-K slabs, no reduce launch), and the LayerNorm in front of the QKV,
@@ -979,7 +996,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
     // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
     const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
-    if (fused && !w8 && (c->quant || (small_m_steps() && n_tok <= 32)) && gemm_small_ok(n_tok, d, true) &&
+    if (fused && !w8 && ((c->quant && n_tok <= quant_small_max()) || (small_m_steps() && n_tok <= 32)) && gemm_small_ok(n_tok, d, true) &&
         gemm_small_ok(n_tok, 4 * d, false)) {
         decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
         return;
@@ -1136,6 +1153,9 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
     const int gsz = cdiv(n_tok, groups);
     DecView half[2];
     dec_halves(c, s, gsz, xdirect, half[0], half[1]);
+    // block-quantized files: one dequantization scratch per state, so the groups run one after the
+    // other on the state's stream
+    if (c->quant) half[1] = half[0];
     WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
     WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
     for (int g = 0, r0 = 0; r0 < n_tok; g++, r0 += gsz) {

@@ -117,6 +117,16 @@ int launch_gemm_partials(DType dt, const GemmArgs& a, hipStream_t st);
 bool gemm_small_ok(int M, int K, bool lna);
 // out[r][k] (compute type) = the dequantized weights of rows [0, rows) of a block-quantized matrix
 void launch_dequant(DType dt, const QMat& q, long rows, int K, void* out, hipStream_t st);
+// up to 6 matrices of ONE GGML type dequantized by one launch (start[] is filled by the launcher)
+struct DequantJobs {
+    int n = 0;
+    QMat q[6];
+    long rows[6];
+    int K[6];
+    void* out[6];
+    long start[7];
+};
+void launch_dequant_multi(DType dt, DequantJobs J, hipStream_t st);
 void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream_t st);
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------

@@ -1408,6 +1408,44 @@ static void launch_dequant_t(const QMat& q, long rows, int K, T* out, hipStream_
     }
 }
 
+// several matrices of one GGML type in one launch (a decoder layer's six projections: the decode
+// steps of > 32 clips dequantize each layer once per step into the scratch their split-K GEMMs read)
+template <typename T, int QT>
+__global__ void __launch_bounds__(256) dequant_multi_kernel(const DequantJobs J) {
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= J.start[J.n]) return;
+    int j = 0;
+    while (j + 1 < J.n && i >= J.start[j + 1]) j++;
+    const long li = i - J.start[j], per_row = J.K[j] / 8;
+    const long n = li / per_row;
+    const int e = (int)(li - n * per_row) * 8, b = e / 32, g = (e & 31) / 8;
+    *(u32x4*)((T*)J.out[j] + n * J.K[j] + e) = qraw_deq<QT, T>(qraw_load<QT>(J.q[j], n, J.K[j], b, g), g);
+}
+
+template <typename T>
+static void launch_dequant_multi_t(const DequantJobs& J, hipStream_t st) {
+    const unsigned grid = (unsigned)((J.start[J.n] + 255) / 256);
+    switch (J.q[0].type) {
+        case 2: dequant_multi_kernel<T, 2><<<grid, 256, 0, st>>>(J); break;
+        case 3: dequant_multi_kernel<T, 3><<<grid, 256, 0, st>>>(J); break;
+        case 6: dequant_multi_kernel<T, 6><<<grid, 256, 0, st>>>(J); break;
+        case 7: dequant_multi_kernel<T, 7><<<grid, 256, 0, st>>>(J); break;
+        case 8: dequant_multi_kernel<T, 8><<<grid, 256, 0, st>>>(J); break;
+        default: WM_FAIL("dequant: ggml type %d not supported", J.q[0].type);
+    }
+}
+
+void launch_dequant_multi(DType dt, DequantJobs J, hipStream_t st) {
+    if (J.n <= 0) return;
+    J.start[0] = 0;
+    for (int j = 0; j < J.n; j++) {
+        if (J.q[j].type != J.q[0].type || J.K[j] % 32) WM_FAIL("dequant_multi: mixed types or K %% 32");
+        J.start[j + 1] = J.start[j] + J.rows[j] * (J.K[j] / 8);
+    }
+    if (dt == DType::F16) launch_dequant_multi_t<half_t>(J, st);
+    else launch_dequant_multi_t<bf16_t>(J, st);
+}
+
 void launch_dequant(DType dt, const QMat& q, long rows, int K, void* out, hipStream_t st) {
     if (rows <= 0) return;
     if (K % 32) WM_FAIL("dequant: K %% 32 != 0 (K=%d)", K);

@@ -135,12 +135,14 @@ def test_quant_arena_keeps_blocks(wrs, qtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", ["tiny+conf+q5_0", "small-4L+conf+q5_1"])
 def test_quant_batch_equals_single(wrs, monkeypatch, shape):
-    """40 clips (decode steps read the blocks in 32-row chunks) == whisper_full_with_state per clip,
-    bit for bit (cache form): a row's sums do not depend on the rows beside it on this path."""
+    """40 clips with the small-M path forced for every decode step (its GEMMs read the blocks in
+    32-row chunks) == whisper_full_with_state per clip, bit for bit (cache form): a row's sums do not
+    depend on the rows beside it on this path."""
     from conftest import model_path
     from make_model import synthetic_pcm
     from test_gpu_configs import seg_ints
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    monkeypatch.setenv("WHISPER_MI355X_QSMALL_MAX", "64")
     ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
     clips = [synthetic_pcm(k % 12, seconds=30.0 - k % 5) for k in range(40)]
     p = wrs.reference_full_params("en")
@@ -153,4 +155,34 @@ def test_quant_batch_equals_single(wrs, monkeypatch, shape):
         assert st.full(p, clips[j]) == 0
         assert seg_ints(st.segments()) == batch[j], j
         st.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cross", ["direct", "cache"])
+@pytest.mark.parametrize("shape,clip", [("tiny+conf+q5_0", 1), ("large-v3-2L+conf+q5_0", 0)])
+def test_quant_batch_dequant_path_exact(wrs, monkeypatch, cross, shape, clip):
+    """Decode steps of more than 32 clips of a quantized file dequantize each layer's blocks once per
+    step (one launch) and run the split-K GEMMs: 40 clips, the oracle's exact case at rows 0, 33 and 39,
+    each equal to the oracle (f16, exact; the same bar as test_quant_full_f16_exact)."""
+    from conftest import model_path
+    from make_model import synthetic_pcm
+    from oracle_py import reference_params
+    from test_gpu_configs import ref_ints, seg_ints
+    pcm = synthetic_pcm(clip)
+    o = Oracle(model_path(shape), mode=1, n_threads=16)
+    ref = o.full(pcm, reference_params("en"))
+    o.close()
+    assert min(ref["margins"]) > F16_GAP
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", cross)
+    ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
+    rows = (0, 33, 39)
+    clips = [pcm if j in rows else synthetic_pcm(j % 12 + 2, seconds=30.0 - j % 5) for j in range(40)]
+    st = ctx.create_state()
+    assert st.full_batch(wrs.reference_full_params("en"), clips) == 0
+    for j in rows:
+        segs = st.batch_segments(j)
+        assert seg_ints(segs) == ref_ints(ref), j
+        assert [s.text for s in segs] == [s["text"] for s in ref["segments"]], j
+    st.close()
     ctx.close()
