@@ -814,17 +814,19 @@ struct DecView {
     float *xo, *xml;
 };
 
-// The small-M decode path (decoder_rows_small) is what block-quantized files run (its GEMM reads the
-// blocks); for f16 / bf16 weights it is opt-in (WHISPER_MI355X_SMALLM=1): measured slower than the
-// split-K path at 16 clips (profiles/r03_prof16_smallm{0,1}.md, large-v3 bf16: 101 vs 94 us per
-// decoder layer). Its 80 workgroups of 16 columns pull the weights more slowly than split-K's 200-240,
-// and the LayerNorm recomputed by every workgroup costs ~4.7 us per LN-consuming GEMM.
-static bool small_m_steps() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_SMALLM");
-        return e && atoi(e) == 1;
-    }();
-    return on;
+// The small-M decode path (decoder_rows_small): every projection one launch (no split-K slabs, no
+// reduce launch), LayerNorm in the GEMM prologue. Default for decode steps of <= 4 clips: at one clip
+// base f16 471-481 -> 539-540 audio-s/s, large-v3 f16 78 -> 80 (profiles/r03_smallm_b1_ab.txt); at 16
+// clips it measured slower (large-v3 bf16: 101 vs 94 us per decoder layer, r03_prof16_smallm{0,1}.md:
+// its 80 workgroups of 16 columns pull the weights more slowly than split-K's 200-240, and the
+// LayerNorm recomputed by every workgroup costs ~4.7 us per LN-consuming GEMM at 16 rows).
+// WHISPER_MI355X_SMALLM=0 off, =1 up to 32 clips, =k up to k clips (read per call). Block-quantized
+// files use it up to quant_small_max() clips whatever this says.
+static int small_m_max() {
+    const char* e = getenv("WHISPER_MI355X_SMALLM");
+    if (!e) return 4;
+    const int v = atoi(e);
+    return v == 1 ? 32 : std::max(0, std::min(32, v));
 }
 
 // Decode steps of block-quantized files: up to this many clips the small-M path reads the blocks
@@ -996,7 +998,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
     // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
     const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
-    if (fused && !w8 && ((c->quant && n_tok <= quant_small_max()) || (small_m_steps() && n_tok <= 32)) && gemm_small_ok(n_tok, d, true) &&
+    if (fused && !w8 && ((c->quant && n_tok <= quant_small_max()) || n_tok <= small_m_max()) && gemm_small_ok(n_tok, d, true) &&
         gemm_small_ok(n_tok, 4 * d, false)) {
         decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
         return;
