@@ -14,4 +14,4 @@ run() {
 }
 run bf16 --batch 32 --tokens 4 --steps 1 --warmup 1 --cpu-baseline 0 &&
 run fp8 --model large-v3-turbo --dtype fp8 --batch 32 --tokens 4 --steps 1 --warmup 1 --cpu-baseline 0 &&
-python3 "$R/tools/pmc_mfma.py"
+python3 "$R/tools/pmc_mfma.py" "${1:-r02}"

@@ -19,8 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def read(counter: str, d: str):
+    """d: a directory, or a glob of directories (one per workload: pmc_fetch_b128, pmc_fetch_b16, ...)"""
     acc = defaultdict(lambda: [0, 0.0])
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    files = []
+    for dd in sorted(glob.glob(d)):
+        files += glob.glob(os.path.join(dd, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         sys.exit(f"no counter_collection.csv under {d}")
     for f in files:
@@ -36,8 +39,8 @@ def read(counter: str, d: str):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    fetch = read("FETCH_SIZE", os.path.join(ROOT, "gpurun_out", "pmc_fetch"))
-    write = read("WRITE_SIZE", os.path.join(ROOT, "gpurun_out", "pmc_write"))
+    fetch = read("FETCH_SIZE", os.path.join(ROOT, "gpurun_out", "pmc_fetch*"))
+    write = read("WRITE_SIZE", os.path.join(ROOT, "gpurun_out", "pmc_write*"))
     out = {}
     for k in sorted(set(fetch) | set(write)):
         nf, f = fetch.get(k, (0, 0.0))
