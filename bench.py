@@ -368,6 +368,8 @@ def main():
     ap.add_argument("--variants", type=int, default=1,
                     help="also time the reference's prompted (default vocabulary) and auto-language workloads")
     ap.add_argument("--variant-steps", type=int, default=3)
+    ap.add_argument("--inflight-line", type=int, default=1,
+                    help="with --variants: also a serving line with two batches in flight (two states)")
     ap.add_argument("--fallback-line", type=int, default=0,
                     help="also time the reference's verbatim FullParams with temperature fallback (slow on "
                          "untrained weights: most windows fall back to sampled re-decodes)")
@@ -540,6 +542,37 @@ def main():
                                  decoded_tokens_per_chunk=round(dec_tok / max(1, nb), 1),
                                  windows=sum(len(st.decisions(j)) for j in range(nb)), windows_fallen_back=fell_back,
                                  phase_ms_last_step={k: round(v, 1) for k, v in st.phase_ms().items()}))
+
+        # serving mode: two batches of the same chunks in flight at once, on two whisper_states (each
+        # with its own HIP streams and decode graphs) driven from two host threads (ctypes releases the
+        # GIL): one batch's launch chain runs in the other's latency gaps. Not the headline (that is one
+        # 128-chunk batch at a time, BASELINE configs[3]); tools/overlap_probe.py has the offsets.
+        if args.inflight_line and nb:
+            import threading
+            st2 = ctx.create_state()
+            rc2 = [0]
+
+            def step2():
+                rc2[0] = st2.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
+            step2()
+            step(params)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(args.variant_steps):
+                th = threading.Thread(target=step2)
+                th.start()
+                step(params)
+                th.join()
+                assert rc2[0] == 0, rc2[0]
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.time() - t0, dist, "cuda")
+            variants.append(dict(workload=f"serving: 2 batches of {global_batch} chunks in flight (two states on two "
+                                          f"streams, two host threads), fixed {args.tokens}-token decode, language en",
+                                 value=round(2 * 30.0 * global_batch * args.variant_steps / el, 2),
+                                 ms_per_batch=round(1e3 * el / (2 * args.variant_steps), 2), batches_in_flight=2))
+            st2.close()
 
     frontend = None
     if args.frontend and rank == 0 and nb:
