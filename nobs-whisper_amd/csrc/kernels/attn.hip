@@ -486,6 +486,18 @@ __global__ void __launch_bounds__(512) attn_enc3_kernel(const T* __restrict__ qk
         }
 }
 
+// Sums over the 8 lanes of a key row by DPP (quad xor 1, quad xor 2, half-row mirror): the same bits as
+// the xor butterfly (after two steps every lane of a quad holds the quad sum), without LDS round trips.
+template <int CTRL>
+__device__ __forceinline__ float dpp8_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8(float a) {
+    a += dpp8_f<0xB1>(a);
+    a += dpp8_f<0x4E>(a);
+    return a + dpp8_f<0x141>(a);
+}
+
 // ------------------------------------------------------------------------------------------------
 // FQ: q is not read from a buffer but reduced from the cross-Q projection's split-K slabs
 // (DecSlabs; q = (T)((sum_z + bias) * scale), the EPI_STORE epilogue of that GEMM).
@@ -550,9 +562,7 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
             float a = 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-            a += __shfl_xor(a, 1);
-            a += __shfl_xor(a, 2);
-            a += __shfl_xor(a, 4);
+            a = sum8(a);  // DPP, no ds_bpermute round trips (same bits as the xor butterfly)
             if (t < n_kv) {
                 if (lane8 == 0) sc[t] = a;
                 lmax = fmaxf(lmax, a);
@@ -659,15 +669,6 @@ __global__ void __launch_bounds__(256) attn_cross_step_kernel(const DecSlabs sl,
 // Sums over the 8 lanes of a key row by DPP (quad xor 1, quad xor 2, half-row mirror): the same
 // bits as the xor butterfly, without LDS round trips. NT: the cached K and V rows (read once per
 // step) by non-temporal loads.
-template <int CTRL>
-__device__ __forceinline__ float dpp8_f(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float sum8(float a) {
-    a += dpp8_f<0xB1>(a);
-    a += dpp8_f<0x4E>(a);
-    return a + dpp8_f<0x141>(a);
-}
 template <typename T, int HPB, bool NT>
 __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs sl, T* __restrict__ cache,
                                                                   const int* __restrict__ slot,
