@@ -292,7 +292,7 @@ static void free_ws(Workspace& w) {
     // are freed with their parent
     dfree(w.mel_img); dfree(w.h1); dfree(w.hn); dfree(w.qkv); dfree(w.att); dfree(w.ff); dfree(w.x);
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
-    dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.win_job);
+    dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
     dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.mxs); dfree(w.qtiles); dfree(w.wdq);
     if (w.h_ints) hipHostFree(w.h_ints);
@@ -377,7 +377,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         const int L = hp.n_text_layer;
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
-        dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.mel_ptrs);
+        dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.mel_ptrs);
         dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles);
         for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
             if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
@@ -411,6 +411,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         w.lrows = w.tok + 5 * n_tok;
         dalloc(w.ctl, (size_t)n_jobs * sizeof(SeqCtl));
         dalloc(w.tout, (size_t)n_jobs * sizeof(TokOut));
+        dalloc(w.lrec, logits_rec_bytes(n_jobs));
         dalloc(w.mel_ptrs, (size_t)n_jobs * (2 * sizeof(void*) + 3 * sizeof(int)));
         w.pcm_ptrs = (const float**)(w.mel_ptrs + n_jobs);
         w.n_samp = (int*)(w.pcm_ptrs + n_jobs);
@@ -1483,7 +1484,7 @@ static bool logits_prepare(Sched& S, const std::vector<int>& act, bool want_nosp
 static void logits_launch(Context* c, whisper_state* s, int n) {
     Workspace& w = s->ws;
     KT kt(s, K_LOGITS, (double)n * c->hp.n_vocab * 4);
-    launch_logits(w.logits, c->hp.n_vocab, w.ctl, n, c->vid, w.tout, w.probs, s->stream);
+    launch_logits(w.logits, c->hp.n_vocab, w.ctl, n, c->vid, w.tout, w.probs, w.lrec, s->stream);
 }
 static void logits_finish(Sched& S, int n, bool any_probs, std::vector<std::vector<float>>& probs_rows) {
     Context* c = S.c;

@@ -157,6 +157,7 @@ struct Workspace {
     int *tok = nullptr, *pos = nullptr, *slot = nullptr, *nkv_self = nullptr, *nkv_cross = nullptr, *lrows = nullptr;
     SeqCtl* ctl = nullptr;
     TokOut* tout = nullptr;
+    void* lrec = nullptr;  // split logits kernel: per-chunk records
     int *win_job = nullptr, *win_seek = nullptr, *win_slot = nullptr;
     // mel / pcm
     float* pcm = nullptr;

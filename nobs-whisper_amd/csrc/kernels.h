@@ -192,7 +192,10 @@ struct SeqCtl {             // per-sequence inputs of whisper_process_logits
     int want_probs, want_nosp;
 };
 struct TokOut { int id, tid; float p, plog, pt, ptsum, nosp_prob, pad; };
+// rec: scratch of logits_rec_bytes(n_seq) bytes for the split form (rows spread over several workgroups
+// each, used for up to 16 rows); null = one workgroup per row
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v,
-                   TokOut* out, float* probs, hipStream_t st);
+                   TokOut* out, float* probs, void* rec, hipStream_t st);
+size_t logits_rec_bytes(int n_seq);
 
 }  // namespace wm

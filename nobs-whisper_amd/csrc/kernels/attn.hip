@@ -501,20 +501,21 @@ __device__ __forceinline__ float sum8(float a) {
 // ------------------------------------------------------------------------------------------------
 // FQ: q is not read from a buffer but reduced from the cross-Q projection's split-K slabs
 // (DecSlabs; q = (T)((sum_z + bias) * scale), the EPI_STORE epilogue of that GEMM).
-template <typename T, bool FQ>
+template <typename T, bool FQ, int NTH = 256, int U = 8>
 __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_stride, const DecSlabs sl,
                                               const T* __restrict__ cache, const int* __restrict__ slot,
                                               const int* __restrict__ n_kv_arr, int L, int layer, int H, int ctx, int d,
                                               T* __restrict__ out) {
     const int i = blockIdx.x, h = blockIdx.y;
-    const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3;  // 32 groups of 8 lanes
+    constexpr int NG = NTH / 8, NW = NTH / 64;
+    const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3;  // NG groups of 8 lanes
     const int n_kv = n_kv_arr[i];
     const long s = slot[i];
     const T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
     const T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
     __shared__ float sc[1536];
-    __shared__ float red[256];
-    __shared__ float acc_s[32][65];
+    __shared__ float red[NTH];
+    __shared__ float acc_s[NG][65];
 
     // Loads: U key rows per lane group per chunk, the next chunk issued before the current one is
     // consumed (two chunks in flight); the first K chunk is issued before q is formed (it does not
@@ -522,12 +523,12 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     // (per-key sums, the block max, the sum tree, P rounded to T, the P.V order per lane group) is
     // the round-2 kernel's: the sum keeps its tree association (lanes t, t+64, t+128, t+192 first,
     // then halving inside one wave), with 2 barriers instead of 9.
-    constexpr int U = 8, CHR = 32 * U;
+    constexpr int CHR = NG * U;
     const u32x4 zero = {0, 0, 0, 0};
     auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int t = t0 + 32 * u;
+            const int t = t0 + NG * u;
             raw[u] = t < n_kv ? *(const u32x4*)(base + (long)t * 64 + lane8 * 8) : zero;
         }
     };
@@ -557,7 +558,7 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     auto scores = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int t = t0 + 32 * u;
+            const int t = t0 + NG * u;
             const T* ke = (const T*)&raw[u];
             float a = 0.0f;
 #pragma unroll
@@ -585,24 +586,33 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
     if (lane == 0) red[wave] = lmax;
     __syncthreads();
-    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float mx = red[0];
+#pragma unroll
+    for (int w = 1; w < NW; w++) mx = fmaxf(mx, red[w]);
     float lsum = 0.0f;
-    for (int t = tid; t < n_kv; t += 256) {
+    for (int t = tid; t < n_kv; t += NTH) {
         const float e = expf(sc[t] - mx);
         sc[t] = e;
         lsum += e;
     }
-    __syncthreads();  // every wave has read red[0..3]
+    __syncthreads();  // every wave has read red[0..NW)
     red[tid] = lsum;
     __syncthreads();
     if (wave == 0) {
-        float r = (red[lane] + red[lane + 128]) + (red[lane + 64] + red[lane + 192]);
+        float r;
+        if constexpr (NTH == 256) {
+            r = (red[lane] + red[lane + 128]) + (red[lane + 64] + red[lane + 192]);
+        } else {  // wider workgroups (few clips): the waves' partials in wave order
+            r = red[lane];
+#pragma unroll
+            for (int w = 1; w < NW; w++) r = r + red[lane + 64 * w];
+        }
         for (int o = 32; o > 0; o >>= 1) r = r + __shfl_down(r, o);
         if (lane == 0) red[0] = r;
     }
     __syncthreads();
     const float inv = 1.0f / red[0];
-    for (int t = tid; t < n_kv; t += 256) sc[t] = (float)(T)(sc[t] * inv);  // P rounded as ggml's f16 src1
+    for (int t = tid; t < n_kv; t += NTH) sc[t] = (float)(T)(sc[t] * inv);  // P rounded as ggml's f16 src1
     __syncthreads();
     // phase 3: O = P.V
     float acc[8];
@@ -611,7 +621,7 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     auto pv = [&](int t0, const u32x4 (&raw)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int t = t0 + 32 * u;
+            const int t = t0 + NG * u;
             const T* ve = (const T*)&raw[u];
             const float p = t < n_kv ? sc[t] : 0.0f;
 #pragma unroll
@@ -633,7 +643,7 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     __syncthreads();
     if (tid < 64) {
         float a = 0.0f;
-        for (int g2 = 0; g2 < 32; g2++) a += acc_s[g2][tid];
+        for (int g2 = 0; g2 < NG; g2++) a += acc_s[g2][tid];
         out[(long)i * d + h * 64 + tid] = (T)a;
     }
 }
@@ -659,6 +669,16 @@ __global__ void __launch_bounds__(256) attn_cross_step_kernel(const DecSlabs sl,
                                                               const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
                                                               int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
     attn_dec_body<T, true>(nullptr, 0, sl, cache, slot, n_kv_arr, L, layer, H, ctx, d, out);
+}
+// decode steps of few clips (<= 4: the app's one clip per call; n x H workgroups leave most CUs idle):
+// 1024 threads (128 lane groups) per (clip, head), so each pass over the 1500 cached keys is 2-3 memory
+// round trips instead of 6; the sum of the softmax adds the waves' partials in wave order (another
+// association than the 256-thread tree: results can differ in the last bits between the two widths)
+template <typename T>
+__global__ void __launch_bounds__(1024) attn_cross_step_wide_kernel(const DecSlabs sl, const T* __restrict__ cache,
+                                                                    const int* __restrict__ slot, const int* __restrict__ n_kv_arr,
+                                                                    int L, int layer, int H, int ctx, int d, T* __restrict__ out) {
+    attn_dec_body<T, true, 1024, 4>(nullptr, 0, sl, cache, slot, n_kv_arr, L, layer, H, ctx, d, out);
 }
 
 // Decode-step self attention, one wave per (token, head), HPB heads per workgroup. The prologue
@@ -1003,11 +1023,25 @@ void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache
 #undef WM_ATTN_DEC
 }
 
+// WHISPER_MI355X_XWIDE_MAX (default 4, read per call): decode steps of up to this many clips use the
+// 1024-thread cache-form kernel
+static int cross_wide_max() {
+    const char* e = getenv("WHISPER_MI355X_XWIDE_MAX");
+    return e ? atoi(e) : 4;
+}
+
 void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
                             int L, int layer, int H, int ctx, int d, void* out, hipStream_t st) {
     if (n <= 0) return;
     if (ctx > 1536) WM_FAIL("attention context %d > 1536", ctx);
     dim3 grid(n, H);
+    if (n <= cross_wide_max()) {
+        if (dt == DType::F16)
+            attn_cross_step_wide_kernel<half_t><<<grid, 1024, 0, st>>>(sl, (const half_t*)cache, slot, n_kv, L, layer, H, ctx, d, (half_t*)out);
+        else
+            attn_cross_step_wide_kernel<bf16_t><<<grid, 1024, 0, st>>>(sl, (const bf16_t*)cache, slot, n_kv, L, layer, H, ctx, d, (bf16_t*)out);
+        return;
+    }
     if (dt == DType::F16)
         attn_cross_step_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)cache, slot, n_kv, L, layer, H, ctx, d, (half_t*)out);
     else

@@ -235,10 +235,200 @@ __global__ void __launch_bounds__(LT) logits_kernel(const float* __restrict__ lo
     }
 }
 
+// ---- split form for few rows (decode steps of <= 16 clips: one 1024-thread workgroup per row leaves
+// the chip idle and took 38 us per step at one clip) -------------------------------------------------
+// Pass 1: KS workgroups per row, each over a chunk of the vocabulary, write per-chunk statistics of
+// the filtered logits x: the max m over all tokens, over the timestamp tokens (m_ts) and over the text
+// tokens (m_text), the argmax of all and of the timestamp tokens (lowest index on ties), and the sums
+// s = sum exp(x - m), s_ts = sum_ts exp(x - m_ts) (and for no_speech the raw logits' max and sum).
+// Pass 2: one workgroup per row combines them in chunk order: lse = log(sum_c s_c e^(m_c - M)) + M,
+// the timestamp rule log(S_ts) + M_ts > M_text with S_ts = sum_c s_ts_c e^(m_ts_c - M_ts) (the
+// log-softmax shift cancels out of it), the argmax of p = e^(x - lse) as the argmax of x, and
+// sum_ts p = S_ts e^(M_ts - lse). The same decisions as logits_kernel; sums associate differently (last
+// bits of p, plog, pt), and a near-tie of p under rounding resolves by x instead of by index.
+// want_probs rows (sampled attempts) have pass 2 write the probs / logprobs rows as well.
+static constexpr int KS = 16, LT2 = 256;
+struct LogitRec {
+    float m_r, s_r, m, s, m_ts, s_ts, m_text;
+    int ix_all, ix_ts, pad;
+};
+
+size_t logits_rec_bytes(int n_seq) { return (size_t)std::max(1, n_seq) * KS * sizeof(LogitRec); }
+
+__device__ __forceinline__ void argmax_pair(float& v, int& ix, float ov, int oi) {
+    if (ov > v || (ov == v && oi < ix)) { v = ov; ix = oi; }
+}
+
+template <int NW>
+__device__ float blk_max(float x, float* sh) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < NW; i++) r = fmaxf(r, sh[i]);
+    return r;
+}
+template <int NW>
+__device__ float blk_sum(float x, float* sh) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    float r = 0.0f;
+    for (int i = 0; i < NW; i++) r += sh[i];
+    return r;
+}
+template <int NW>
+__device__ void blk_argmax(float& v, int& ix, float* shv, int* shi) {
+    for (int o = 32; o > 0; o >>= 1) argmax_pair(v, ix, __shfl_xor(v, o), __shfl_xor(ix, o));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { shv[threadIdx.x >> 6] = v; shi[threadIdx.x >> 6] = ix; }
+    __syncthreads();
+    v = shv[0]; ix = shi[0];
+    for (int i = 1; i < NW; i++) argmax_pair(v, ix, shv[i], shi[i]);
+}
+
+__global__ void __launch_bounds__(LT2) logits_part_kernel(const float* __restrict__ logits, long ld,
+                                                          const SeqCtl* __restrict__ ctl, VocabIds v,
+                                                          LogitRec* __restrict__ rec) {
+    constexpr int NW = LT2 / 64, PER = 14;  // 14 * 256 * 16 >= 51866
+    const int c = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, n = v.n_vocab;
+    const SeqCtl q = ctl[s];
+    const float* L = logits + (long)s * ld;
+    const int cs = (n + KS - 1) / KS, i0 = c * cs, i1 = min(n, i0 + cs);
+    __shared__ float shf[NW];
+    __shared__ int shi[NW];
+    float raw[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = i0 + tid + k * LT2;
+        raw[k] = i < i1 ? L[i] : -INFINITY;
+    }
+    LogitRec r;
+    r.m_r = -INFINITY; r.s_r = 0.0f; r.pad = 0;
+    if (q.want_nosp) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < PER; k++) mx = fmaxf(mx, raw[k]);
+        mx = blk_max<NW>(mx, shf);
+        float sm = 0.0f;
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (i0 + tid + k * LT2 < i1) sm += __expf(raw[k] - mx);
+        r.m_r = mx;
+        r.s_r = blk_sum<NW>(sm, shf);
+    }
+    float m = -INFINITY, mts = -INFINITY, mtx = -INFINITY;
+    int ix = 0x7fffffff, its = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = i0 + tid + k * LT2;
+        const float x = i < i1 ? masked_logit(raw[k], i, q, v) : -INFINITY;
+        raw[k] = x;
+        if (x > -INFINITY) {
+            argmax_pair(m, ix, x, i);
+            if (i >= v.beg) argmax_pair(mts, its, x, i);
+            else mtx = fmaxf(mtx, x);
+        }
+    }
+    blk_argmax<NW>(m, ix, shf, shi);
+    blk_argmax<NW>(mts, its, shf, shi);
+    mtx = blk_max<NW>(mtx, shf);
+    float sm = 0.0f, sts = 0.0f;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = i0 + tid + k * LT2;
+        if (raw[k] > -INFINITY) {
+            sm += __expf(raw[k] - m);
+            if (i >= v.beg) sts += expf(raw[k] - mts);
+        }
+    }
+    r.m = m; r.m_ts = mts; r.m_text = mtx; r.ix_all = ix; r.ix_ts = its;
+    r.s = blk_sum<NW>(sm, shf);
+    r.s_ts = blk_sum<NW>(sts, shf);
+    if (tid == 0) rec[(long)s * KS + c] = r;
+}
+
+__global__ void __launch_bounds__(LT2) logits_combine_kernel(const float* __restrict__ logits, long ld,
+                                                             const SeqCtl* __restrict__ ctl, VocabIds v,
+                                                             const LogitRec* __restrict__ rec, TokOut* __restrict__ out,
+                                                             float* __restrict__ probs) {
+    const int s = blockIdx.x, tid = threadIdx.x, n = v.n_vocab;
+    const SeqCtl q = ctl[s];
+    const float* L = logits + (long)s * ld;
+    __shared__ float sh_lse;
+    __shared__ int sh_mask;
+    if (tid == 0) {
+        const LogitRec* R = rec + (long)s * KS;
+        float M = -INFINITY, Mts = -INFINITY, Mtx = -INFINITY, Mr = -INFINITY;
+        int ix = 0x7fffffff, its = 0x7fffffff;
+        for (int c = 0; c < KS; c++) {
+            argmax_pair(M, ix, R[c].m, R[c].ix_all);
+            argmax_pair(Mts, its, R[c].m_ts, R[c].ix_ts);
+            Mtx = fmaxf(Mtx, R[c].m_text);
+            Mr = fmaxf(Mr, R[c].m_r);
+        }
+        float S = 0.0f, Sts = 0.0f, Sr = 0.0f;
+        for (int c = 0; c < KS; c++) {
+            if (R[c].m > -INFINITY) S += R[c].s * expf(R[c].m - M);
+            if (R[c].m_ts > -INFINITY) Sts += R[c].s_ts * expf(R[c].m_ts - Mts);
+            if (q.want_nosp && R[c].m_r > -INFINITY) Sr += R[c].s_r * expf(R[c].m_r - Mr);
+        }
+        const float lse = logf(S) + M;
+        const float mts = Mts - lse, mtext = Mtx - lse;
+        const float ts_logprob = Sts > 0.0f ? logf(Sts) + mts : -INFINITY;
+        const bool mask_text = ts_logprob > mtext;
+        TokOut r;
+        const float xb = mask_text ? Mts : M;
+        const int ib = mask_text ? its : ix;
+        const float best = xb > -INFINITY ? __expf(xb - lse) : 0.0f;
+        r.id = best > 0.0f ? ib : 0;
+        r.p = best;
+        {
+            float xv = masked_logit(L[r.id], r.id, q, v);
+            if (mask_text && r.id < v.beg) xv = -INFINITY;
+            r.plog = xv > -INFINITY ? xv - lse : -INFINITY;
+        }
+        const float best_ts = Mts > -INFINITY ? __expf(Mts - lse) : 0.0f;
+        const double sum_ts = Mts > -INFINITY ? (double)Sts * (double)expf(Mts - lse) : 0.0;
+        r.tid = best_ts > 0.0f ? its : 0;
+        r.pt = (float)((double)best_ts / (sum_ts + 1e-10));
+        r.ptsum = (float)sum_ts;
+        if (r.id >= v.beg) { r.tid = r.id; r.pt = r.p; }
+        r.nosp_prob = q.want_nosp ? expf(L[v.nosp] - (logf(Sr) + Mr)) : 0.0f;
+        r.pad = 0.0f;
+        out[s] = r;
+        sh_lse = lse;
+        sh_mask = mask_text;
+    }
+    if (!q.want_probs) return;
+    __syncthreads();
+    const float lse = sh_lse;
+    const bool mask_text = sh_mask;
+    for (int i = tid; i < n; i += LT2) {
+        float xv = masked_logit(L[i], i, q, v);
+        if (mask_text && i < v.beg) xv = -INFINITY;
+        probs[(long)s * 2 * n + i] = xv == -INFINITY ? 0.0f : __expf(xv - lse);
+        probs[(long)s * 2 * n + n + i] = xv == -INFINITY ? -INFINITY : xv - lse;
+    }
+}
+
+// WHISPER_MI355X_LOGITS_SPLIT_MAX (default 16, read per call): rows up to this count take the split form
+static int logits_split_max() {
+    const char* e = getenv("WHISPER_MI355X_LOGITS_SPLIT_MAX");
+    return e ? atoi(e) : 16;
+}
+
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v, TokOut* out, float* probs,
-                   hipStream_t st) {
+                   void* rec, hipStream_t st) {
     if (n_seq <= 0) return;
     if (v.n_vocab > NPT * LT) WM_FAIL("vocabulary %d > %d", v.n_vocab, NPT * LT);
+    if (rec && n_seq <= logits_split_max() && v.n_vocab <= 14 * LT2 * KS) {
+        logits_part_kernel<<<dim3(KS, n_seq), LT2, 0, st>>>(logits, ld, ctl, v, (LogitRec*)rec);
+        logits_combine_kernel<<<n_seq, LT2, 0, st>>>(logits, ld, ctl, v, (const LogitRec*)rec, out, probs);
+        return;
+    }
     logits_kernel<<<n_seq, LT, (size_t)NPT_LDS * LT * sizeof(float), st>>>(logits, ld, ctl, v, out, probs);
 }
 
