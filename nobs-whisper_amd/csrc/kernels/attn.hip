@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
-    constexpr int U = 4;
+    constexpr int U = 8;
     const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
     for (int t0 = grp; t0 < pos; t0 += 8 * U) {
