@@ -1453,6 +1453,28 @@ void launch_dequant(DType dt, const QMat& q, long rows, int K, void* out, hipStr
     else launch_dequant_t<bf16_t>(q, rows, K, (bf16_t*)out, st);
 }
 
+// sum of a double over TPR consecutive lanes (TPR = 16 or 32, aligned groups), the same value in each:
+// within 16 lanes by DPP (quad xor 1, quad xor 2, half-row mirror, row mirror: VALU, no LDS), then for
+// TPR = 32 one xor-16 exchange. Used by the LayerNorm prologue of gemm_small_kernel (double sums, as
+// ggml_norm), where six dependent ds_bpermute rounds per sum were most of the prologue.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int TPR>
+__device__ __forceinline__ double row_sum_f64(double v) {
+    static_assert(TPR == 16 || TPR == 32, "16- or 32-lane rows");
+    v += dpp_f64<0xB1>(v);
+    v += dpp_f64<0x4E>(v);
+    v += dpp_f64<0x141>(v);
+    v += dpp_f64<0x140>(v);
+    if constexpr (TPR == 32) v += __shfl_xor(v, 16);
+    return v;
+}
+
 // Decode steps of <= 32 active clips (the app's one clip per call, whisper.rs:83-85; one rank's shard
 // of configs[3] at 8 GPUs): one workgroup = 16 output columns x all M rows x the whole K. Its 8 waves
 // split K (wave w: the 32-wide K-steps w, w + 8, ...) and add their partial sums in LDS in wave order, so no
@@ -1512,7 +1534,7 @@ __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < NJ; j++) s += (((double)v[j].x + (double)v[j].y) + (double)v[j].z) + (double)v[j].w;
-        for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        s = row_sum_f64<TPR>(s);
         const float mean = (float)(s / K);
         double s2 = 0.0;
 #pragma unroll
@@ -1523,7 +1545,7 @@ __global__ void __launch_bounds__(512) gemm_small_kernel(const GemmArgs g) {
                       (double)(v[j].w * v[j].w);
             }
         }
-        for (int o = TPR / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+        s2 = row_sum_f64<TPR>(s2);
         const float scale = 1.0f / sqrtf((float)(s2 / K) + 1e-5f);
         T* ar = aimg + (long)r * lda;
 #pragma unroll

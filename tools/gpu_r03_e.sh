@@ -12,7 +12,7 @@ fi
 Q="--variants 0 --frontend 0 --cpu-baseline 0 --app-pattern 0"
 for B in ${BATCHES:-16 128}; do
   for v in ${VERS:-old mid new old mid new}; do
-    timeout -k 10 300 env WHISPER_MI355X_LIB=$R/nobs-whisper_amd/lib_ab/$v.so python -u bench.py --global-batch $B --steps 3 --warmup 1 $Q \
+    timeout -k 10 300 env WHISPER_MI355X_LIB=$R/nobs-whisper_amd/lib_ab/$v.so python -u bench.py --global-batch $B --steps ${STEPS:-3} --warmup 1 $Q $MODEL_ARGS \
       > gpurun_out/lab_${B}_$v.json 2> gpurun_out/lab_${B}_$v.err
     rc=$?; [ $rc -eq 0 ] || { echo "bench $B $v rc=$rc"; tail -5 gpurun_out/lab_${B}_$v.err; exit $rc; }
     python3 -c "import json; d=json.loads(open('gpurun_out/lab_${B}_$v.json').read().strip().splitlines()[-1]); r=d['roofline']; print('B=$B', '$v'.ljust(5), d['value'], d['extra']['phase_ms_last_step'], r['kernel'], round(r['avg_launch_ms']*1e3, 1))"
