@@ -11,6 +11,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 #include "engine.h"
 
@@ -215,6 +217,10 @@ whisper_state* new_state(Context* c) {
 static void free_ws(Workspace& w);
 
 static void destroy_state(whisper_state* s) {
+    if (s->twin) {
+        destroy_state(s->twin);
+        s->twin = nullptr;
+    }
     if (Context* c = s->ctx) {
         std::lock_guard<std::mutex> lk(c->pool_mu);
         c->live.erase(std::remove(c->live.begin(), c->live.end(), s), c->live.end());
@@ -1580,8 +1586,60 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     kt_flush_graph(s, *G);
 }
 
+// Batches above WHISPER_MI355X_PAIR_MIN clips (default 128; 0 = off) run as two independent halves at
+// once: the first on this state, the second on a twin state (its own streams, workspace and decode
+// graphs, kept with this state for later calls) from a second host thread, and the twin's per-clip
+// results are appended. Each half is exactly a batch of its own clips (the same bits as two separate
+// calls), and one half's launch chain runs in the other's latency gaps: two 128-chunk large-v3 batches
+// in flight measured 3720 vs 3201 audio-s/s back to back (profiles/r03_overlap_two_batches.txt),
+// where one 256-row decode step ran as two lockstep row groups before.
+static int pair_min() {
+    const char* e = getenv("WHISPER_MI355X_PAIR_MIN");  // read per call
+    return e ? atoi(e) : 128;
+}
+
+static int full_batch_one(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
+                          int n_jobs, bool on_device, const FullOpts& o, bool single_api);
+
 int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                int n_jobs, bool on_device, const FullOpts& o, bool single_api) {
+    const int pm = pair_min();
+    if (single_api || pm <= 0 || n_jobs <= pm) return full_batch_one(c, s, p, pcm, n, n_jobs, on_device, o, single_api);
+    WM_CHECK(hipSetDevice(c->device));
+    if (!s->twin) s->twin = create_state(c);
+    whisper_state* t = s->twin;
+    const int na = (n_jobs + 1) / 2;
+    int ra = 0, rb = 0;
+    std::exception_ptr ea, eb;
+    std::thread th([&] {
+        try {
+            rb = full_batch_one(c, t, p, pcm + na, n + na, n_jobs - na, on_device, o, false);
+        } catch (...) {
+            eb = std::current_exception();
+        }
+    });
+    try {
+        ra = full_batch_one(c, s, p, pcm, n, na, on_device, o, false);
+    } catch (...) {
+        ea = std::current_exception();
+    }
+    th.join();
+    if (eb) recover_state(t);
+    if (ea) std::rethrow_exception(ea);
+    if (eb) std::rethrow_exception(eb);
+    if (ra) return ra;
+    if (rb) return rb;
+    for (int j = 0; j < n_jobs - na; j++) {
+        s->results.push_back(std::move(t->results[j]));
+        s->lang_ids.push_back(t->lang_ids[j]);
+        s->decisions.push_back(std::move(t->decisions[j]));
+    }
+    s->decoded_tokens += t->decoded_tokens;
+    return 0;
+}
+
+static int full_batch_one(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
+                          int n_jobs, bool on_device, const FullOpts& o, bool single_api) {
     WM_CHECK(hipSetDevice(c->device));
     if (p.strategy != WHISPER_SAMPLING_GREEDY) {
         fprintf(stderr, "whisper_mi355x: beam search is not implemented (the reference uses Greedy, whisper.rs:88)\n");

@@ -220,6 +220,7 @@ struct whisper_state {
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step
+    whisper_state* twin = nullptr;                // second half of a paired batch (full_batch)
 };
 
 struct whisper_context {
