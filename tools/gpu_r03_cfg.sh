@@ -7,10 +7,10 @@ cd "$R" && mkdir -p gpurun_out
 X="--variants 0 --frontend 0 --app-pattern 0"
 run() {
     local tag=$1; shift
-    timeout -k 10 600 python bench.py "$@" > "gpurun_out/cfg3_$tag.json" 2> "gpurun_out/cfg3_$tag.err"
+    timeout -k 10 600 python bench.py "$@" > "gpurun_out/cfgc_$tag.json" 2> "gpurun_out/cfgc_$tag.err"
     local rc=$?; echo "$tag rc=$rc"
-    [ $rc -eq 0 ] || { tail -5 "gpurun_out/cfg3_$tag.err"; return $rc; }
-    python3 -c "import json; d=json.loads(open('gpurun_out/cfg3_$tag.json').read().strip().splitlines()[-1]); r=d['roofline']; print('  ', d['value'], d['extra']['phase_ms_last_step'], r['kernel'], r['frac'], (d.get('cpu_baseline') or {}).get('value'))"
+    [ $rc -eq 0 ] || { tail -5 "gpurun_out/cfgc_$tag.err"; return $rc; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/cfgc_$tag.json').read().strip().splitlines()[-1]); r=d['roofline']; print('  ', d['value'], d['extra']['phase_ms_last_step'], r['kernel'], r['frac'], (d.get('cpu_baseline') or {}).get('value'))"
 }
 run base_f16_b1 --model base --dtype f16 --global-batch 1 --steps 10 --warmup 2 $X &&
 run small_bf16_b32 --model small --global-batch 32 --steps 2 --warmup 1 $X &&
