@@ -789,14 +789,12 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, 
 }
 
 // decode steps, direct cross attention: WHISPER_MI355X_XQ_FUSED=1 fuses the cross-Q GEMM's split-K
-// reduce into the Q' projection (launch_xattn_qproj_slabs, bit-identical). Off by default: one launch
-// fewer per layer, but decode 843 vs 823 ms per step at 128 clips (profiles/r03_envab_xq_xowt.txt)
-static bool xq_fused() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_XQ_FUSED");
-        return e && atoi(e) != 0;
-    }();
-    return on;
+// reduce into the Q' projection (launch_xattn_qproj_slabs, bit-identical; d % 256 == 0, d <= 1280).
+// Read per call. Off by default: one launch fewer per layer, but decode 855 vs 848 ms per step at 128
+// clips (profiles/r03_envab_xq_gelu.txt; the first form, 20 serial L2 round trips per wave, 843 vs 823).
+static bool xq_fused(int d) {
+    const char* e = getenv("WHISPER_MI355X_XQ_FUSED");
+    return e && atoi(e) != 0 && d % 256 == 0 && d <= 1280;
 }
 
 // WHISPER_MI355X_XSERP=1: odd decoder layers read each clip's encoder rows in reverse order, so that
@@ -1049,7 +1047,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             // -> one pass over E per clip -> split merge + Wv. Decode steps: the cross-Q GEMM leaves
             // split-K slabs that the Q' projection reduces itself (one launch fewer per layer)
             const void* wkt_l = (const char*)W.wkT + (size_t)lw * H * d * 64 * 2;
-            if (fused && xq_fused()) {
+            if (fused && xq_fused(d)) {
                 const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);
                 KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * d * sl.splits + 4.0 * n_tok * H * d, st);
                 launch_xattn_qproj_slabs(dt, sl, wkt_l, n_tok, d, H, c->k_scale, qx, st);

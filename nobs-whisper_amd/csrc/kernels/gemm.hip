@@ -1685,6 +1685,12 @@ void launch_gemm_small(DType dt, int epi, const GemmArgs& g, bool lna, hipStream
 
 int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
 static int dec_splits_override() { return g_dec_splits; }
+// WHISPER_MI355X_DEC_GELU_SPLITS=k (tuning, read per call): the decode-step GELU GEMM (FC1) with at most
+// k splits (1 = unsplit, the GELU in the GEMM's epilogue and no reduce launch); 0/unset = dec_splits_for
+static int dec_gelu_splits() {
+    const char* e = getenv("WHISPER_MI355X_DEC_GELU_SPLITS");
+    return e ? std::max(0, atoi(e)) : 0;
+}
 // decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU; default), or
 // with WHISPER_MI355X_DEC_FILL=0 the smallest reaching >= 160; both with chunks of >= 2 K-tiles and
 // at most WHISPER_MI355X_DEC_MAXS (12) splits. Independent of M, so a row's sums never depend on the
@@ -1781,6 +1787,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int mch = cdiv(g.M, 128);
         int splits = dec_splits_for(tiles, nk);
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
+        if (EPI == EPI_GELU && dec_gelu_splits() > 0) splits = std::min(splits, dec_gelu_splits());
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
         const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64 && !g.w8_scale;

@@ -135,27 +135,49 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
         }
 }
 
-// Q' projection fused with the cross-Q GEMM's split-K reduce (decode steps): grid (H, cdiv(n, 16)),
+// Q' projection fused with the cross-Q GEMM's split-K reduce (decode steps): grid (H, cdiv(n, 16), 4),
 // 256 threads. The workgroup first reduces q_h for its 16 tokens from the slabs, exactly as
 // splitk_reduce_kernel<EPI_STORE> would (sum over splits in order from 0, + bias, * scale, rounded to
-// T), into an LDS image; then wave w computes columns [w*d/4, (w+1)*d/4) of Q'_h for the 16 tokens
-// with the same MFMA operands and order as xattn_qproj_kernel (A = Wk_h^T rows, B = q_h, K = 64):
-// the outputs are bit-identical to the reduce + qproj pair, one launch and one round trip fewer.
+// T; every split's piece loaded at once), into an LDS image; then wave w computes 80 columns of its
+// quarter of Q'_h (blockIdx.z) for the 16 tokens, every Wk_h^T fragment loaded before the first MFMA,
+// with the same MFMA operands and order as xattn_qproj_kernel (A = Wk_h^T rows, B = q_h, K = 64): the
+// outputs are bit-identical to the reduce + qproj pair, one launch and one round trip fewer. (The first
+// form, one workgroup per (head, 16 tokens) walking 320 columns per wave, chained 20 L2 round trips.)
 template <typename T>
 __global__ void __launch_bounds__(256) xattn_qproj_slabs_kernel(const DecSlabs sl, const T* __restrict__ wkt, int n, int d,
                                                                 int H, float scale, T* __restrict__ qx) {
     typedef typename Frag<T>::type FT;
-    const int h = blockIdx.x, i0 = blockIdx.y * 16;
+    const int h = blockIdx.x, i0 = blockIdx.y * 16, cq = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ __attribute__((aligned(16))) T qimg[16 * 64];
+    constexpr int MT = 5;  // 16-column tiles per wave (d <= 1280: d / 16 columns per quarter per wave)
+    const int cpw = d / 16, c0 = cq * (d / 4) + wave * cpw;  // this wave's columns (d % 256 == 0)
+    const int nmt = cpw / 16;
+    // Wk_h^T fragments of this wave's columns, in flight under the slab reduce
+    FT af[MT][2];
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) {
+        const int cr = c0 + mt * 16 + (lane & 15);
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++)
+            af[mt][ks] = mt < nmt ? __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + cr) * 64 + ks * 32 + 8 * (lane >> 4)))
+                                  : af[0][0];
+    }
     {
         const int tk = tid >> 4, c = h * 64 + (tid & 15) * 4, i = i0 + tk;
         T o[4] = {(T)0.0f, (T)0.0f, (T)0.0f, (T)0.0f};
         if (i < n) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int z = 0; z < sl.splits; z++) {
-                const float4 w = *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c);
-                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+            const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 w[16];
+#pragma unroll
+            for (int z = 0; z < 16; z++) w[z] = z < sl.splits ? *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c) : zero4;
+            float4 v = zero4;
+#pragma unroll
+            for (int z = 0; z < 16; z++)
+                if (z < sl.splits) { v.x += w[z].x; v.y += w[z].y; v.z += w[z].z; v.w += w[z].w; }
+            for (int z = 16; z < sl.splits; z++) {  // WHISPER_MI355X_DEC_SPLITS above 16 only
+                const float4 u = *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c);
+                v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
             }
             const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -171,17 +193,13 @@ __global__ void __launch_bounds__(256) xattn_qproj_slabs_kernel(const DecSlabs s
     FT bq[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ks++) bq[ks] = __builtin_bit_cast(FT, *(const u32x4*)&qimg[(lane & 15) * 64 + ks * 32 + 8 * (lane >> 4)]);
-    const int cpw = d / 4, c0 = wave * cpw;  // columns of this wave (multiple of 16: d % 64 == 0)
     const int i = i0 + (lane & 15);
-    for (int mt = 0; mt < cpw / 16; mt++) {
-        const int cr = c0 + mt * 16 + (lane & 15);
-        FT af[2];
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++)
-            af[ks] = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + cr) * 64 + ks * 32 + 8 * (lane >> 4)));
+    for (int mt = 0; mt < MT; mt++) {
+        if (mt >= nmt) break;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[ks], bq[ks], acc);
+        for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[mt][ks], bq[ks], acc);
         if (i >= n) continue;
         const int c = c0 + mt * 16 + 4 * (lane >> 4);
         T hi[4], lo[4];
@@ -573,8 +591,8 @@ void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, 
 void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
                               hipStream_t st) {
     if (n <= 0) return;
-    if (d % 64 || sl.ld % 4) WM_FAIL("fused Q' projection: d %d", d);
-    dim3 grid(H, cdiv(n, 16));
+    if (d % 256 || d > 1280 || sl.ld % 4) WM_FAIL("fused Q' projection: d %d", d);
+    dim3 grid(H, cdiv(n, 16), 4);
     if (dt == DType::F16)
         xattn_qproj_slabs_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
     else
