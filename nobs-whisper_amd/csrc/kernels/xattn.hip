@@ -447,26 +447,33 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
 }
 
 // ---- merge the splits and apply Wv ---------------------------------------------------------------
-// grid (H, cdiv(n, 16)), 512 threads. Phase A (every thread, coalesced 16-byte partial reads): the
-// merged E~ = sum_s w_s O_s / L of 16 tokens x d columns, split into hi / lo rows of an LDS image
-// [32][d] (16-byte chunks XOR-swizzled by row). Phase B: wave w takes the 32-column k-steps
-// w, w+8, ...: M = 32 (hi, lo rows), N = 64 outputs, Wv rows straight from global (L2-shared by the
+// grid (H, cdiv(n, TOK)), 512 threads. Phase A (every thread, coalesced 16-byte partial reads): the
+// merged E~ = sum_s w_s O_s / L of TOK tokens x d columns, split into hi / lo rows of an LDS image
+// [2 TOK][d] (16-byte chunks XOR-swizzled by row). Phase B: wave w takes the 32-column k-steps
+// w, w+8, ...: M = 2 TOK (hi, lo rows), N = 64 outputs, Wv rows straight from global (L2-shared by the
 // head's token blocks); the 8 waves' partial products are summed through LDS.
+// TOK = 8 (the default): one 16-row MFMA tile holds the hi and lo rows, and twice the workgroups fill
+// the chip (160 -> 320 at 128 clips); every output is bit-identical to TOK = 16 (each MFMA output row
+// is its own dot product; the final sum keeps the wave order, hi before lo).
 // m is in log2 units (the step kernel scales scores by log2 e).
-template <typename T>
+template <typename T, int TOK>
 __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restrict__ opart, const float* __restrict__ ml,
                                                             int splits, const T* __restrict__ wv, const float* __restrict__ bv,
                                                             int n, int d, int H, T* __restrict__ out) {
     typedef typename Frag<T>::type FT;
     constexpr int DMAX = 1280;
-    const int h = blockIdx.x, i0 = blockIdx.y * 16;
+    // 16-row A tiles: (hi 0-15, lo 16-31) for TOK = 16, (hi 0-7, lo 8-15) for 8, (hi 0-3, lo 4-7, rows
+    // 8-15 unused: MFMA output rows are independent) for 4
+    constexpr int NA = TOK >= 8 ? TOK / 8 : 1, RT = 16 * NA;
+    const int h = blockIdx.x, i0 = blockIdx.y * TOK;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    __shared__ __attribute__((aligned(16))) char lds[32 * DMAX * 2 + 16 * 16 * 4];
-    T* aimg = (T*)lds;                           // [32][d]: rows 0-15 hi, 16-31 lo
-    float* red = (float*)lds;                    // after phase B: [8 waves][32][64] (reuses aimg)
-    float* wgt = (float*)(lds + 32 * DMAX * 2);  // [16 tokens][16 splits]
+    __shared__ __attribute__((aligned(16))) char lds[RT * DMAX * 2 + TOK * 16 * 4];
+    T* aimg = (T*)lds;                           // [RT][d]: rows 0..TOK-1 hi, TOK..2 TOK-1 lo
+    float* red = (float*)lds;                    // after phase B: [8 waves][RT][64] (reuses aimg)
+    float* wgt = (float*)(lds + RT * DMAX * 2);  // [TOK tokens][16 splits]
+    static_assert(8 * RT * 64 * 4 <= RT * DMAX * 2, "reduce image fits the A image");
     auto slot_of = [&](int row, int ch) { return row * d + ((ch & ~15) | ((ch & 15) ^ (row & 15))) * 8; };
-    if (tid < 16) {
+    if (tid < TOK) {
         const int i = i0 + tid;
         if (i < n) {
             const float* p = ml + ((long)i * splits * H + h) * 2;
@@ -497,13 +504,13 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
     __syncthreads();
     // the partial sums of all NE chunks of a split in flight at once (split order per element kept)
     const int q4 = d / 4;
-    constexpr int NE = 16 * (DMAX / 4) / 512;
+    constexpr int NE = (TOK * (DMAX / 4) + 511) / 512;
     float4 a[NE];
     const float* src[NE];
 #pragma unroll
     for (int j = 0; j < NE; j++) {
         a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int e = min(tid + 512 * j, 16 * q4 - 1);
+        const int e = min(tid + 512 * j, TOK * q4 - 1);
         const int t = e / q4, c = (e - t * q4) * 4;
         src[j] = opart + ((long)min(i0 + t, n - 1) * splits * H + h) * d + c;
     }
@@ -513,7 +520,7 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         for (int j = 0; j < NE; j++) x[j] = *(const float4*)(src[j] + (long)s * H * d);
 #pragma unroll
         for (int j = 0; j < NE; j++) {
-            const int t = min(tid + 512 * j, 16 * q4 - 1) / q4;
+            const int t = min(tid + 512 * j, TOK * q4 - 1) / q4;
             const float w = wgt[t * 16 + s];
             a[j].x += w * x[j].x; a[j].y += w * x[j].y; a[j].z += w * x[j].z; a[j].w += w * x[j].w;
         }
@@ -521,7 +528,7 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
 #pragma unroll
     for (int j = 0; j < NE; j++) {
         const int e = tid + 512 * j;
-        if (e >= 16 * q4) break;
+        if (e >= TOK * q4) break;
         const int t = e / q4, c = (e - t * q4) * 4;
         const float v[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
         T hi[4], lo[4];
@@ -532,40 +539,39 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         }
         const int ch = c >> 3, half = ((c >> 2) & 1) * 4;
         *(uint2*)(aimg + slot_of(t, ch) + half) = *(const uint2*)hi;
-        *(uint2*)(aimg + slot_of(16 + t, ch) + half) = *(const uint2*)lo;
+        *(uint2*)(aimg + slot_of(TOK + t, ch) + half) = *(const uint2*)lo;
     }
     __syncthreads();
-    f32x4 acc[2][4];
+    f32x4 acc[NA][4];
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+    for (int a = 0; a < NA; a++)
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[a][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
         const int ks = wave + 8 * k;
         if (ks >= d / 32) break;  // wave-uniform
-        const FT ahi = *(const FT*)(aimg + slot_of(r16, ks * 4 + kq));
-        const FT alo = *(const FT*)(aimg + slot_of(16 + r16, ks * 4 + kq));
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            acc[0][j] = mfma16x16x32(ahi, bfp[k][j], acc[0][j]);
-            acc[1][j] = mfma16x16x32(alo, bfp[k][j], acc[1][j]);
+        for (int a = 0; a < NA; a++) {
+            const FT af = *(const FT*)(aimg + slot_of(a * 16 + r16, ks * 4 + kq));
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[a][j] = mfma16x16x32(af, bfp[k][j], acc[a][j]);
         }
     }
     __syncthreads();  // every wave is done with aimg
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+    for (int a = 0; a < NA; a++)
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) red[(wave * 32 + a * 16 + 4 * kq + r) * 64 + j * 16 + r16] = acc[a][j][r];
+            for (int r = 0; r < 4; r++) red[(wave * RT + a * 16 + 4 * kq + r) * 64 + j * 16 + r16] = acc[a][j][r];
     __syncthreads();
-    for (int e = tid; e < 16 * 64; e += 512) {
+    for (int e = tid; e < TOK * 64; e += 512) {
         const int ti = e >> 6, j = e & 63;
         if (i0 + ti >= n) continue;
         float v = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 8; w++) v += red[(w * 32 + ti) * 64 + j] + red[(w * 32 + 16 + ti) * 64 + j];
+        for (int w = 0; w < 8; w++) v += red[(w * RT + ti) * 64 + j] + red[(w * RT + TOK + ti) * 64 + j];
         out[(long)(i0 + ti) * d + h * 64 + j] = (T)(v + bv[h * 64 + j]);
     }
 }
@@ -640,11 +646,22 @@ void launch_xattn_combine(DType dt, const float* opart, const float* ml, int spl
                           int d, int H, void* out, hipStream_t st) {
     if (n <= 0) return;
     if (splits > 16 || d % 128 || d > 1280) WM_FAIL("combine shape not supported");
-    dim3 grid(H, cdiv(n, 16));
-    if (dt == DType::F16)
-        xattn_combine_kernel<half_t><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
-    else
-        xattn_combine_kernel<bf16_t><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
+    // tokens per workgroup: WHISPER_MI355X_XCOMB_TOK = 4 / 8 / 16 (read per call); every choice gives the
+    // same bits. Default: 8 (twice the round-2 grid).
+    const char* e = getenv("WHISPER_MI355X_XCOMB_TOK");
+    const int tok = e ? atoi(e) : 8;
+#define WM_XCOMB(TOK_)                                                                                                       \
+    do {                                                                                                                     \
+        dim3 grid(H, cdiv(n, TOK_));                                                                                         \
+        if (dt == DType::F16)                                                                                                \
+            xattn_combine_kernel<half_t, TOK_><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out); \
+        else                                                                                                                 \
+            xattn_combine_kernel<bf16_t, TOK_><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out); \
+    } while (0)
+    if (tok == 16) WM_XCOMB(16);
+    else if (tok == 4) WM_XCOMB(4);
+    else WM_XCOMB(8);
+#undef WM_XCOMB
 }
 
 }  // namespace wm
