@@ -87,36 +87,37 @@ __device__ __forceinline__ float sum16(float x) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---- Q' projection -----------------------------------------------------------------------------
-// grid (cdiv(d, 256), H, cdiv(n, 64)), 256 threads: wave w = columns [256x + 64w, +64) x 64 tokens,
-// K = 64. Swapped product C^T[c][tok] = Wk_h^T[c][:] . q_h[tok][:]: a lane holds 4 consecutive
-// columns of one token, stored as one 8-byte hi and one 8-byte lo write.
-template <typename T>
+// grid (cdiv(d, 64 MT), H, cdiv(n, 16 NT)), 256 threads: wave w = columns [64 MT x + 16 MT w, +16 MT) x
+// 16 NT tokens, K = 64. Swapped product C^T[c][tok] = Wk_h^T[c][:] . q_h[tok][:]: a lane holds 4
+// consecutive columns of one token, stored as one 8-byte hi and one 8-byte lo write. Every (MT, NT)
+// gives the same bits (one MFMA pair per 16 x 16 tile whatever the tiling).
+template <typename T, int MT, int NT>
 __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ q, const T* __restrict__ wkt, int n, int d,
                                                           int H, float scale, T* __restrict__ qx) {
     typedef typename Frag<T>::type FT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int c0 = blockIdx.x * 256 + wave * 64, h = blockIdx.y, i0 = blockIdx.z * 64;
+    const int c0 = blockIdx.x * 64 * MT + wave * 16 * MT, h = blockIdx.y, i0 = blockIdx.z * 16 * NT;
     if (c0 >= d) return;  // wave-uniform
     const u32x4 zero = {0, 0, 0, 0};
-    FT af[4][2], bq[4][2];
+    FT af[MT][2], bq[NT][2];
 #pragma unroll
-    for (int mt = 0; mt < 4; mt++) {
+    for (int mt = 0; mt < MT; mt++) {
         const int c = c0 + mt * 16 + (lane & 15);
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
             af[mt][ks] = __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + c) * 64 + ks * 32 + 8 * (lane >> 4)));
     }
 #pragma unroll
-    for (int nt = 0; nt < 4; nt++) {
+    for (int nt = 0; nt < NT; nt++) {
         const int i = i0 + nt * 16 + (lane & 15);
 #pragma unroll
         for (int ks = 0; ks < 2; ks++)
             bq[nt][ks] = __builtin_bit_cast(FT, i < n ? *(const u32x4*)(q + (long)i * d + h * 64 + ks * 32 + 8 * (lane >> 4)) : zero);
     }
 #pragma unroll
-    for (int mt = 0; mt < 4; mt++)
+    for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-        for (int nt = 0; nt < 4; nt++) {
+        for (int nt = 0; nt < NT; nt++) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[mt][ks], bq[nt][ks], acc);
@@ -587,11 +588,24 @@ bool xattn_supported(int d) { return d == 384 || d == 512 || d == 768 || d == 10
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st) {
     if (n <= 0) return;
-    dim3 grid(cdiv(d, 256), H, cdiv(n, 64));
-    if (dt == DType::F16)
-        xattn_qproj_kernel<half_t><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
-    else
-        xattn_qproj_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
+    // tile per wave: WHISPER_MI355X_XQP_TILE = 24 (32 columns x 64 tokens, default: twice the workgroups of
+    // the round-2 shape), 44 (64 x 64, round 2), 42, 22 (read per call; the same bits for each). 24 vs 44:
+    // 64-clip shard 2340-2352 vs 2314-2330 audio-s/s, 128 clips neutral (profiles/r03_xcomb_tok_ab.txt)
+    const char* e = getenv("WHISPER_MI355X_XQP_TILE");
+    const int tile = e ? atoi(e) : 24;
+#define WM_XQP(MT_, NT_)                                                                                                     \
+    do {                                                                                                                     \
+        dim3 grid(cdiv(d, 64 * MT_), H, cdiv(n, 16 * NT_));                                                                  \
+        if (dt == DType::F16)                                                                                                \
+            xattn_qproj_kernel<half_t, MT_, NT_><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx); \
+        else                                                                                                                 \
+            xattn_qproj_kernel<bf16_t, MT_, NT_><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx); \
+    } while (0)
+    if (tile == 44) WM_XQP(4, 4);
+    else if (tile == 42) WM_XQP(4, 2);
+    else if (tile == 22) WM_XQP(2, 2);
+    else WM_XQP(2, 4);
+#undef WM_XQP
 }
 
 void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
