@@ -688,7 +688,7 @@ int whisper_mi355x_debug_quant_fp8(struct whisper_context* ctx, const void* x, l
 int whisper_mi355x_debug_attn_encoder(struct whisper_context* ctx, const void* qkv, int B, int T, int d, int H,
                                       int variant, void* out, int reps, float* ms) {
     return guarded(nullptr, [&]() -> int {
-        if (!ctx || B < 1 || T < 1 || d != 64 * H || variant < 1 || variant > 5 || variant == 4) return -1;
+        if (!ctx || B < 1 || T < 1 || d != 64 * H || variant < 1 || variant > 6 || variant == 4) return -1;
         hipSetDevice(ctx->c.device);
         hipStream_t st;
         WM_CHECK(hipStreamCreate(&st));

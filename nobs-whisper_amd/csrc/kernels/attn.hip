@@ -163,11 +163,15 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(const T* __restrict__ qkv
 //                             the permuted key order of that layout), A = V^T via
 //                             ds_read_b64_tr_b16 from a row-major V image (no transposing store)
 // Exponentials in base 2 with the 1/8 scale and log2(e) folded into one FMA.
-// MINW = 4 (variant 5, the default): the register allocation held to 128 VGPRs so that two workgroups
+// MINW = 4 (variant 5; with PK = false variant 6, the default): the register allocation held to 128 VGPRs so that two workgroups
 // share a CU (4 waves per SIMD); they drift apart between their barriers, so one workgroup's softmax
 // runs beside the other's MFMAs: 578 vs 694 us per 32-window large-v3 launch (random bf16 operands,
 // profiles/r03_attn_encoder_variants.txt). MINW = 1 (variant 2): 138 VGPRs, one workgroup per CU.
-template <typename T, int MINW = 1>
+// PK = false (variant 6): the exponent arguments and row sums as scalar v_fma_f32 / v_add_f32 (inline asm,
+// so the compiler cannot re-pack them) instead of v_pk_fma_f32 / v_pk_add_f32, which the guide prices
+// above two scalar ops beside MFMAs; the same per-element operations, so the same bits. No VGPR spill at
+// 128 (variant 5: 2); encode 325.9 -> 324.6 ms per step at 128 clips (profiles/r03_attn_encoder_variants.txt).
+template <typename T, int MINW = 1, bool PK = true>
 __global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
     typedef typename Frag<T>::type FT;
     typedef short v4s __attribute__((ext_vector_type(4)));
@@ -272,19 +276,40 @@ __global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restric
         const f2 c2 = {c, c}, nm2 = {-m_new, -m_new};
         FT pf[4];
         f2 ls2 = {0.0f, 0.0f};
+        if constexpr (PK) {
 #pragma unroll
-        for (int kb = 0; kb < 2; kb++)
+            for (int kb = 0; kb < 2; kb++)
 #pragma unroll
-            for (int sp = 0; sp < 2; sp++)
+                for (int sp = 0; sp < 2; sp++)
 #pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    const f2 x = {sacc[kb][sp * 8 + j], sacc[kb][sp * 8 + j + 1]};
-                    const f2 e = __builtin_elementwise_fma(x, c2, nm2);
-                    const f2 p = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-                    ls2 += p;
-                    pf[kb * 2 + sp][j] = (T)p.x;
-                    pf[kb * 2 + sp][j + 1] = (T)p.y;
-                }
+                    for (int j = 0; j < 8; j += 2) {
+                        const f2 x = {sacc[kb][sp * 8 + j], sacc[kb][sp * 8 + j + 1]};
+                        const f2 e = __builtin_elementwise_fma(x, c2, nm2);
+                        const f2 p = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+                        ls2 += p;
+                        pf[kb * 2 + sp][j] = (T)p.x;
+                        pf[kb * 2 + sp][j + 1] = (T)p.y;
+                    }
+        } else {
+            const float nm = -m_new;
+            float lx = 0.0f, ly = 0.0f;
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+                for (int sp = 0; sp < 2; sp++)
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2) {
+                        float ex, ey;
+                        asm("v_fma_f32 %0, %1, %2, %3" : "=v"(ex) : "v"(sacc[kb][sp * 8 + j]), "v"(c), "v"(nm));
+                        asm("v_fma_f32 %0, %1, %2, %3" : "=v"(ey) : "v"(sacc[kb][sp * 8 + j + 1]), "v"(c), "v"(nm));
+                        const float px = __builtin_amdgcn_exp2f(ex), py = __builtin_amdgcn_exp2f(ey);
+                        asm("v_add_f32 %0, %1, %2" : "=v"(lx) : "v"(lx), "v"(px));
+                        asm("v_add_f32 %0, %1, %2" : "=v"(ly) : "v"(ly), "v"(py));
+                        pf[kb * 2 + sp][j] = (T)px;
+                        pf[kb * 2 + sp][j + 1] = (T)py;
+                    }
+            ls2 = f2{lx, ly};
+        }
         l_run = l_run * alpha + (ls2.x + ls2.y);
         if (moved) {
 #pragma unroll
@@ -980,13 +1005,19 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
                          int variant_arg) {
     static const int variant_env = [] {
         const char* e = getenv("WHISPER_MI355X_ATTN");
-        return e ? atoi(e) : 5;
+        return e ? atoi(e) : 6;
     }();
     const int variant = variant_arg >= 0 ? variant_arg : variant_env;
     if (variant == 3 && d == H * 64) {
         dim3 grid(cdiv(Tn, 256), H, B);
         if (dt == DType::F16) attn_enc3_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
         else attn_enc3_kernel<bf16_t><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
+        return;
+    }
+    if (variant == 6 && d == H * 64) {
+        dim3 grid(cdiv(Tn, 256), H, B);
+        if (dt == DType::F16) attn_enc2_kernel<half_t, 4, false><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
+        else attn_enc2_kernel<bf16_t, 4, false><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
         return;
     }
     if (variant == 5 && d == H * 64) {

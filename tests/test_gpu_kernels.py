@@ -227,7 +227,8 @@ def _attn_run(wrs, ctx, qkv_dev, B, T, d, H, variant, reps=0):
 def test_attn_encoder_pipelined_equals_enc2(wrs, micro_model, dtype, B, T, H):
     """Every encoder-attention variant == attn_enc2_kernel bit for bit (same per-element operations and
     order): 3 = score MFMAs of the next key tile issued under the softmax of the current one, 5 = variant 2
-    held to 128 VGPRs (two workgroups per CU, the default); and variant 2 against a float64
+    held to 128 VGPRs (two workgroups per CU), 6 = 5 with scalar instead of packed f32 exponent arguments
+    and row sums (the default); and variant 2 against a float64
     softmax(Q K^T / 8) V of the same rounded operands."""
     c = wrs.WhisperContext(micro_model, dtype=getattr(wrs, dtype))
     d = 64 * H
@@ -242,7 +243,7 @@ def test_attn_encoder_pipelined_equals_enc2(wrs, micro_model, dtype, B, T, H):
     p = _dev(wrs, c, np.ascontiguousarray(bits))
     o2, _ = _attn_run(wrs, c, p, B, T, d, H, 2)
     bad = {}
-    for v in (3, 5):  # every variant: the same per-element operations in the same order
+    for v in (3, 5, 6):  # every variant: the same per-element operations in the same order
         ov, _ = _attn_run(wrs, c, p, B, T, d, H, v)
         if not np.array_equal(o2, ov):
             bad[v] = int((o2 != ov).sum())
@@ -273,7 +274,7 @@ def test_attn_encoder_variant_timing(wrs, micro_model):
     flop = 4.0 * B * H * T * T * 64
     ref = None
     line = []
-    for v in (2, 3, 5, 2, 5):
+    for v in (2, 3, 5, 6, 2, 5, 6):
         o, ms = _attn_run(wrs, c, p, B, T, d, H, v, reps=5)
         line.append(f"v{v} {ms * 1e3:.1f} us {flop / ms / 1e9:.0f} TF/s")
         ref = o if ref is None else ref
