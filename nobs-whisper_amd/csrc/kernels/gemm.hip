@@ -1750,6 +1750,16 @@ static int gemm_group_m() {
     return v;
 }
 
+// the plain split-K reduce of a decode step: one thread per 4 columns (N % 4 == 0), 64-thread
+// workgroups when that is under 64K threads so the work spreads over every CU (at 128 clips a d-wide
+// reduce is 41K threads: 160 busy 256-thread workgroups before, 640 of 64 now); the same bits
+template <typename T, int EPI>
+static void launch_splitk_reduce(const GemmArgs& g, int splits, hipStream_t st) {
+    const long total = (long)g.M * g.N, work = (g.N & 3) == 0 ? total / 4 : total;
+    const int thr = work < 65536 ? 64 : 256;
+    splitk_reduce_kernel<T, EPI><<<std::min<long>(4096, cdiv(work, thr)), thr, 0, st>>>(g, splits);
+}
+
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     if (g.w8_scale) {  // e4m3 weights: the decode-step split-K kernel only
@@ -1807,8 +1817,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
             } else {
-                const long total = (long)g.M * g.N;
-                splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
+                launch_splitk_reduce<T, EPI>(g, splits, st);
             }
             return;
         }
@@ -1832,8 +1841,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
                 else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
                 else WM_FAIL("fused LN width %d > 2048", g.N);
             } else {
-                const long total = (long)g.M * g.N;
-                splitk_reduce_kernel<T, EPI><<<std::min<long>(1024, cdiv(total, 256)), 256, 0, st>>>(g, splits);
+                launch_splitk_reduce<T, EPI>(g, splits, st);
             }
         } else {
             dim3 grid(tiles, 1);
