@@ -128,12 +128,6 @@ WHISPER_API int whisper_mi355x_debug_gemm_fp8(struct whisper_context * ctx, int 
 WHISPER_API int whisper_mi355x_debug_gemm_w8(struct whisper_context * ctx, int epi, const void * A, int M, int K,
                                              const void * B8, const float * b_scale, int N, const float * bias,
                                              void * out, const float * ln_w, const float * ln_b, void * y);
-// MX hand-off of the fp8 encoder: epi 8 (EPI_GELU_MX) writes out = e4m3 bytes [M][N] of GELU(C) with one
-// E8M0 scale per row and 32-column block into mx_scale [M][N/32]; epi 2 (EPI_RESID) with a_scale = NULL
-// reads A as MX e4m3 with those block scales (out f32 [M][N] += C). Device pointers.
-WHISPER_API int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context * ctx, int epi, const void * A8,
-                                                 const float * a_scale, void * mx_scale, int M, int K, const void * B8,
-                                                 const float * b_scale, int N, const float * bias, void * out);
 // q[r][:] = e4m3(x[r][:] / s[r]), s[r] = max|x[r][:]| / 448; x in the context's MFMA type
 WHISPER_API int whisper_mi355x_debug_quant_fp8(struct whisper_context * ctx, const void * x, long rows, int K,
                                                void * q, float * s);

@@ -478,7 +478,7 @@ int whisper_mi355x_phase_ms(struct whisper_state* s, double out[5]) {
 }
 int whisper_mi355x_get_mel(struct whisper_state* s, float* out, int cap) {
     return guarded(nullptr, [&]() -> int {
-        if (!s || !s->ws.mel) return -1;
+        if (!s || !s->ctx || !s->ws.mel) return -1;  // orphan state: its context was freed
         Context* c = s->ctx;
         const int nm = c->hp.n_mels, nl = s->n_len;
         if ((long)nm * nl > cap) return -nm * nl;
@@ -497,7 +497,7 @@ int whisper_mi355x_get_mel(struct whisper_state* s, float* out, int cap) {
 }
 int whisper_mi355x_get_encoder_out(struct whisper_state* s, float* out, int cap) {
     return guarded(nullptr, [&]() -> int {
-        if (!s || !s->ws.hn || s->last_enc_windows < 1) return -1;
+        if (!s || !s->ctx || !s->ws.hn || s->last_enc_windows < 1) return -1;  // orphan state: -1
         Context* c = s->ctx;
         const long n = (long)c->hp.n_audio_ctx * c->hp.n_audio_state;
         if (n > cap) return -1;
@@ -656,23 +656,6 @@ int whisper_mi355x_debug_gemm_w8(struct whisper_context* ctx, int epi, const voi
         launch_gemm(ctx->c.dt, epi, g, nullptr);
         WM_CHECK(hipDeviceSynchronize());
         hipFree(g.splitk_ws);
-        return 0;
-    });
-}
-int whisper_mi355x_debug_gemm_fp8_mx(struct whisper_context* ctx, int epi, const void* A8, const float* a_scale,
-                                     void* mx_scale, int M, int K, const void* B8, const float* b_scale, int N,
-                                     const float* bias, void* out) {
-    return guarded(nullptr, [&]() -> int {
-        if (!ctx || !mx_scale) return -1;
-        hipSetDevice(ctx->c.device);
-        GemmArgs g{};
-        g.A = A8; g.a_rpb = M; g.a_bstride = 0; g.a_rstride = K;
-        g.B = B8; g.bias = bias; g.M = M; g.N = N; g.K = K;
-        g.out = out; g.ldo = N; g.o_rpb = M; g.o_bstride = 0; g.o_off = 0;
-        g.sc_div = 0; g.sc_mod = 1; g.sc_lim = 0; g.scale = 1.0f;
-        g.mx_scale = (uint8_t*)mx_scale;
-        launch_gemm_fp8(ctx->c.dt, epi, g, a_scale, b_scale, nullptr);
-        WM_CHECK(hipDeviceSynchronize());
         return 0;
     });
 }

@@ -83,7 +83,6 @@ struct KT {
 static void drop_graphs(whisper_state* s) {
     for (auto& g : s->dec_graphs) {
         hipGraphExecDestroy(g.exec);
-        if (g.exec2) hipGraphExecDestroy(g.exec2);
         for (auto& e : g.ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     }
     s->dec_graphs.clear();
@@ -125,18 +124,10 @@ void kt_flush(whisper_state* s) {
 // GEMM runs instead of being written back at the kernel boundary before the reduce can start
 // (MI355X_MICROARCH.md price list, "boundary": + dirty bytes / 6 TB/s). Same-box A/B, large-v3 bf16:
 // decode 864 -> 824 ms per step at 128 clips, 423 -> 413 at 16 (profiles/r03_envab_slab_gelu.txt).
-// WHISPER_MI355X_SLAB_WT=0 restores write-back stores.
-static int slab_wt() {
-    static const int on = [] {
-        const char* e = getenv("WHISPER_MI355X_SLAB_WT");
-        return e && atoi(e) == 0 ? 0 : 1;
-    }();
-    return on;
-}
 static void tgemm_ws(whisper_state* s, int cls, DType dt, int epi, const GemmArgs& g0, hipStream_t st, float* ws,
                      long ws_elems) {
     GemmArgs g = g0;
-    if (cls == K_GEMM_DEC) { g.splitk_ws = ws; g.splitk_ws_elems = ws_elems; g.slab_wt = slab_wt(); }
+    if (cls == K_GEMM_DEC) { g.splitk_ws = ws; g.splitk_ws_elems = ws_elems; g.slab_wt = 1; }
     const double work = cls == K_GEMM_ENC ? 2.0 * g.M * g.N * g.K
                                           : 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N;
     KT kt(s, cls, work, st);
@@ -300,7 +291,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.mxs); dfree(w.qtiles); dfree(w.wdq);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
     if (w.h_tout) hipHostFree(w.h_tout);
@@ -319,29 +310,32 @@ static const float kXattnThr = 8.0f;
 // adds two launches per layer (Q' projection, combine); at a few clips a step is launch- and
 // latency-bound and the cached form (one attention kernel, whisper.cpp's own numerics) wins: the
 // cross K/V of a window then costs one GEMM at encode time. WHISPER_MI355X_CROSS=direct|cache
-// forces a form; otherwise direct above WHISPER_MI355X_CROSS_CACHE_MAX (default 32) clips.
+// forces a form; otherwise direct above 32 clips.
 static bool pick_direct(Context* c, int n_jobs) {
     if (!c->cross_direct) return false;
     // read per call (tests switch the form per case)
     const char* e = getenv("WHISPER_MI355X_CROSS");
     if (e && strcmp(e, "direct") == 0) return true;
     if (e && strcmp(e, "cache") == 0) return false;
-    const char* m = getenv("WHISPER_MI355X_CROSS_CACHE_MAX");
-    return n_jobs > (m ? atoi(m) : 32);
+    return n_jobs > 32;
 }
 
-static int enc_batch_cap() {
-    const char* e = getenv("WHISPER_MI355X_ENC_BATCH");
-    int v = e ? atoi(e) : 32;
-    return v > 0 ? v : 32;
-}
+// encoder windows per launch group (32 / 64 / 128 measured the same: 3149-3158 audio-s/s)
+static const int kEncBatch = 32;
 
 // Cross K/V cache for at least `slots` slots (cache form: the call's clips; direct form: the clips
 // whose prompts are too long for the direct prefill). Sized by the calls that use it, so a state
 // that ran a large direct-form batch does not allocate a cache for all of its slots later.
-static void ensure_cross(Context* c, Workspace& w, int slots) {
+// A reallocation drops the state's decode graphs first: a captured cache-form step holds the old
+// w.cross pointer, and the cross cache is sized apart from cap_jobs (a direct-form call of > 32 clips
+// followed by cache-form calls of 8 and then 16 clips regrows it under graphs captured at 8).
+static void ensure_cross(Context* c, whisper_state* s, int slots) {
+    Workspace& w = s->ws;
     if (w.cross && w.cap_cross >= slots) return;
     const Hparams& hp = c->hp;
+    WM_CHECK(hipStreamSynchronize(s->stream));
+    WM_CHECK(hipStreamSynchronize(s->stream2));
+    drop_graphs(s);
     dfree(w.cross);
     w.cap_cross = 0;
     std::fill(w.cross_fresh.begin(), w.cross_fresh.end(), 0);
@@ -350,17 +344,17 @@ static void ensure_cross(Context* c, Workspace& w, int slots) {
 }
 
 // (Re)allocate the workspace for n_jobs clips. Encoder activations are sized for at most
-// enc_batch_cap() windows at once; caches for n_jobs slots. If an allocation fails (out of memory),
+// kEncBatch windows at once; caches for n_jobs slots. If an allocation fails (out of memory),
 // the whole workspace is released and the error propagates: the state stays usable (empty).
 static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
     Workspace& w = s->ws;
     const Hparams& hp = c->hp;
     const size_t d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, E = esize(c->dt);
-    const int n_enc = std::min(n_jobs, enc_batch_cap());
+    const int n_enc = std::min(n_jobs, kEncBatch);
     if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
         dfree(w.mel_img); dfree(w.h1); dfree(w.hn); dfree(w.qkv); dfree(w.att); dfree(w.ff); dfree(w.x);
-        dfree(w.win_job); dfree(w.hs); dfree(w.mxs);
+        dfree(w.win_job); dfree(w.hs);
         w.cap_enc = 0;
         dalloc(w.mel_img, (size_t)n_enc * 3002 * nm * E);
         dalloc(w.h1, (size_t)n_enc * 3002 * d * E);
@@ -372,7 +366,6 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         dalloc(w.x, (size_t)n_enc * T * d * 4);
         if (c->fp8_enc) {
             dalloc(w.hs, (size_t)n_enc * T * sizeof(float));
-            dalloc(w.mxs, (size_t)n_enc * T * (4 * d / 32));
         }
         dalloc(w.win_job, (size_t)n_enc * 3 * sizeof(int));
         w.win_seek = w.win_job + n_enc;
@@ -443,7 +436,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         dalloc(w.xo, xo_rows * H * d * 4);
         dalloc(w.xml, xo_rows * H * 2 * 4);
     }
-    if (!s->direct) ensure_cross(c, w, n_jobs);
+    if (!s->direct) ensure_cross(c, s, n_jobs);
     if (c->quant && !w.wdq) dalloc(w.wdq, (size_t)16 * d * d * E);
 }
 
@@ -592,20 +585,9 @@ static void ensure_fp8(Context* c) {
     c->fp8_ready = true;
 }
 
-// fp8 mode, FC1 -> FC2: MX hand-off (FC1's epilogue quantizes per 32-column block, FC2's block-scaled
-// MFMA takes the scales; no separate quantizer pass over the GELU output). Off by default
-// (WHISPER_MI355X_FP8_MX=1 enables it): measured slower on turbo at 256 clips (encode 743-815 vs
-// 578 ms per step) -- the MX-A FC2 kernel exceeds the 256-VGPR budget of a 2-wave/SIMD tile and
-// spills in its main loop (1091 vs 376 us per launch), and the FC1 MX epilogue costs 67 us more
-// than the bf16 GELU store it replaces; the 78 us requantization pass it removes does not cover either.
-static bool fp8_mx() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_FP8_MX");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
+// fp8 mode, FC1 -> FC2: the GELU output is re-quantized per row (one pass). An MX hand-off (FC1's
+// epilogue quantizing per 32-column block for a block-scaled FC2) measured slower on turbo at 256 clips
+// (encode 743-815 vs 578 ms per step: the MX-A FC2 tile spilled past 256 VGPRs) and was removed.
 static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float* sa, const float* sb, hipStream_t st) {
     KT kt(s, K_GEMM_ENC, 2.0 * g.M * g.N * g.K, st);
     launch_gemm_fp8(s->ctx->dt, epi, g, sa, sb, st);
@@ -615,14 +597,8 @@ static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float*
 // (EPI_GELU), bit-exact with the oracle. bf16: the tanh formula in f32 (EPI_GELU_F; ggml-metal, the
 // reference app's back-end (whisper.rs:40 use_gpu), evaluates GELU by formula too, and the epilogue
 // stages no 75.8 KB table per tile): encode 340 -> 336 ms per step at 128 clips
-// (profiles/r03_envab_slab_gelu.txt). WHISPER_MI355X_GELU_F=0 keeps the table in bf16 too.
-static int enc_gelu_epi(DType dt) {
-    static const bool f = [] {
-        const char* e = getenv("WHISPER_MI355X_GELU_F");
-        return !(e && atoi(e) == 0);
-    }();
-    return dt == DType::BF16 && f ? EPI_GELU_F : EPI_GELU;
-}
+// (profiles/r03_envab_slab_gelu.txt).
+static int enc_gelu_epi(DType dt) { return dt == DType::BF16 ? EPI_GELU_F : EPI_GELU; }
 
 // Projection weights of one layer in the compute type: the arena's matrices, or, for a block-quantized
 // file, the layer's blocks dequantized into the state's scratch (one layer at a time, on the stream
@@ -707,20 +683,9 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
                 }
                 tgemm(s, KCLS, dt, EPI_RESID, gemm_plain(w.att, M, d, L.wo, d, L.bo, w.x, d), st);
                 launch_layernorm_fp8(w.x, M, d, L.ln2_w, L.ln2_b, w.hn, w.hs, st);
-                if (fp8_mx()) {
-                    // FC1 writes its GELU output as MX e4m3 (one E8M0 scale per row and 32-column
-                    // block) straight into the qkv buffer; FC2's block-scaled MFMA consumes the scales
-                    GemmArgs g1 = gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.qkv, 4 * d);
-                    g1.mx_scale = w.mxs;
-                    tgemm_fp8(s, EPI_GELU_MX, g1, w.hs, F.s1, st);
-                    GemmArgs g2 = gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d);
-                    g2.mx_scale = w.mxs;
-                    tgemm_fp8(s, EPI_RESID, g2, nullptr, F.s2, st);
-                } else {
-                    tgemm_fp8(s, EPI_GELU_F, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
-                    launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
-                    tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
-                }
+                tgemm_fp8(s, EPI_GELU_F, gemm_plain(w.hn, M, d, F.w1, 4 * d, L.b1, w.ff, 4 * d), w.hs, F.s1, st);
+                launch_quant_rows_fp8(dt, w.ff, M, 4 * d, w.qkv, w.hs, st);
+                tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
                 continue;
             }
             const LayerMats Wm = layer_mats(c, s, L, st);
@@ -788,26 +753,6 @@ static void decoder_upload(Context* c, whisper_state* s, int n_tok, int n_rows, 
     WM_CHECK(hipMemcpyAsync(w.qtiles, w.h_qtiles, (size_t)nt * sizeof(int2), hipMemcpyHostToDevice, s->stream));
 }
 
-// decode steps, direct cross attention: WHISPER_MI355X_XQ_FUSED=1 fuses the cross-Q GEMM's split-K
-// reduce into the Q' projection (launch_xattn_qproj_slabs, bit-identical; d % 256 == 0, d <= 1280).
-// Read per call. Off by default: one launch fewer per layer, but decode 855 vs 848 ms per step at 128
-// clips (profiles/r03_envab_xq_gelu.txt; the first form, 20 serial L2 round trips per wave, 843 vs 823).
-static bool xq_fused(int d) {
-    const char* e = getenv("WHISPER_MI355X_XQ_FUSED");
-    return e && atoi(e) != 0 && d % 256 == 0 && d <= 1280;
-}
-
-// WHISPER_MI355X_XSERP=1: odd decoder layers read each clip's encoder rows in reverse order, so that
-// the rows a workgroup read last in layer l (still in the 256 MB die-level cache) are read first in
-// layer l + 1 (A/B experiment)
-static bool xattn_serp() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_XSERP");
-        return e && atoi(e) == 1;
-    }();
-    return on;
-}
-
 // One group of decoder rows on one stream: rows [r0, r0+n) of the token arrays and activations,
 // with its own split-K slab region and cross-attention partials, so that two groups can run at the
 // same time (decode steps).
@@ -841,6 +786,11 @@ static int small_m_max() {
 static int quant_small_max() {
     const char* e = getenv("WHISPER_MI355X_QSMALL_MAX");  // read per call (tests switch it)
     return e ? atoi(e) : 32;
+}
+
+// The per-call switches that choose a decode step's kernels, folded into the key of its captured graph.
+static int dec_path_sig() {
+    return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) | (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16);
 }
 
 // Decode step over <= 32 rows (the app's one clip per call, whisper.rs:83-85 / state.rs:147; one
@@ -915,7 +865,7 @@ static void decoder_rows_small(Context* c, whisper_state* s, const DecView& v, b
             }
             {
                 KT kt(s, K_ATTN_CROSS, (double)n * Ta * d * 2, st, kt_layer);
-                launch_xattn_step(dt, w.enc, slot, qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st, xattn_serp() ? (l & 1) : 0);
+                launch_xattn_step(dt, w.enc, slot, qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st);
             }
             {
                 KT kt(s, K_GEMM_DEC, 2.0 * d * d + 4.0 * n * S * d + 2.0 * n * d, st);
@@ -994,7 +944,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         GemmArgs g = use8(gemm_plain(A, n_tok, d, Wt, N, bias, nullptr, N), q8, sc);
         g.splitk_ws = v.splitk;
         g.splitk_ws_elems = v.splitk_elems;
-        g.slab_wt = slab_wt();
+        g.slab_wt = 1;
         KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
         const int splits = launch_gemm_partials(dt, g, st);
         if (splits <= 0) WM_FAIL("decode partials GEMM not applicable");
@@ -1008,17 +958,8 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
         return;
     }
-    // WHISPER_MI355X_DBG_SAMEW=1 (timing experiment only, results are wrong): every decoder layer reads
-    // layer 0's weights, so they stay L2/MALL-hot across the step (upper bound of a weight prefetch).
-    // Measured: decode 856 -> 846 ms per step at 128 clips, 406 -> 403 at 16: the chain is not waiting
-    // for HBM (profiles/r03_envab_decode_cache.txt; a side-branch prefetch of the next layer's weights
-    // made it slower, 1066-1081 ms)
-    static const bool samew = [] {
-        const char* e = getenv("WHISPER_MI355X_DBG_SAMEW");
-        return e && atoi(e) == 1;
-    }();
     for (int l = 0; l < L; l++) {
-        const int lw = samew && fused ? 0 : l;
+        const int lw = l;
         LayerW Lw = W.dec[lw];
         if (c->quant) {  // prefill / language detection: this layer's blocks dequantized into the scratch
             const LayerMats m = layer_mats(c, s, Lw, st);
@@ -1044,14 +985,10 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         resid(datt, d, Lw.wo, Lw.bo, Lw.lnx_w, Lw.lnx_b, F.wo, F.so);
         if (xdirect) {
             // cross attention from the encoder output (kernels/xattn.hip): q -> Q' = s Wk^T q (hi/lo)
-            // -> one pass over E per clip -> split merge + Wv. Decode steps: the cross-Q GEMM leaves
-            // split-K slabs that the Q' projection reduces itself (one launch fewer per layer)
+            // -> one pass over E per clip -> split merge + Wv. (Fusing the cross-Q reduce into the Q'
+            // projection was bit-identical but slower, 855 vs 848 ms per step at 128 clips: removed.)
             const void* wkt_l = (const char*)W.wkT + (size_t)lw * H * d * 64 * 2;
-            if (fused && xq_fused(d)) {
-                const DecSlabs sl = partials(dh, Lw.wxq, d, Lw.bxq, c->k_scale, F.wxq, F.sxq);
-                KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * d * sl.splits + 4.0 * n_tok * H * d, st);
-                launch_xattn_qproj_slabs(dt, sl, wkt_l, n_tok, d, H, c->k_scale, qx, st);
-            } else {
+            {
                 GemmArgs g = use8(gemm_plain(dh, n_tok, d, Lw.wxq, d, Lw.bxq, dq, d), F.wxq, F.sxq);
                 g.scale = c->k_scale; g.sc_div = d; g.sc_mod = 1; g.sc_lim = 1;
                 gemm(KCLS, EPI_STORE, g);
@@ -1062,7 +999,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
             {
                 // the roofline class holds decode steps only (E bytes read once per clip and layer)
                 KT kt(s, fused ? K_ATTN_CROSS : K_OTHER, (double)n_tok * Ta * d * 2, st, kt_layer);
-                launch_xattn_step(dt, w.enc, slot, qx, n_tok, Ta, d, S, kXattnThr, v.xo, v.xml, st, xattn_serp() ? (l & 1) : 0);
+                launch_xattn_step(dt, w.enc, slot, qx, n_tok, Ta, d, S, kXattnThr, v.xo, v.xml, st);
             }
             {
                 KT kt(s, KCLS, 2.0 * d * d + 4.0 * n_tok * S * d + 2.0 * n_tok * d, st);
@@ -1100,18 +1037,11 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
 // branches of the step's hipGraph); two groups for 129..256 clips measured the same as the unfused
 // path in bf16 (turbo at 256 clips: decode 213 vs 217 ms per step) and the fp8 decoder weights exist
 // only on the fused path.
-// WHISPER_MI355X_DEC_STREAMS=2: also split steps of 32..128 clips into two concurrent groups. Off by
-// default: measured slower on large-v3 at 128 clips (2360-2392 vs 2729-2740 audio-s/s; the
-// cross-attention pass at 64 clips per group reads E at 3.6 instead of 4.7 TB/s).
-static int dec_groups(int n_tok) {
-    static const int g = [] {
-        const char* e = getenv("WHISPER_MI355X_DEC_STREAMS");
-        return e ? atoi(e) : 0;
-    }();
-    const int need = cdiv(n_tok, 128);
-    if (g >= 2 && n_tok >= 32) return std::max(2, need);
-    return need;
-}
+// Splitting steps of 32..128 clips into two concurrent groups measured slower on large-v3 at 128 clips
+// (2360-2392 vs 2729-2740 audio-s/s: the cross-attention pass at 64 clips per group reads E at 3.6
+// instead of 4.7 TB/s), and so did two separate graphs on two streams (942 vs 843 ms of decode per
+// step, profiles/r02_dec_groups_ab.txt); both were removed.
+static int dec_groups(int n_tok) { return cdiv(n_tok, 128); }
 
 // The two stream halves of a decode step's scratch: group views on the state's stream use the first
 // half of the split-K slabs and cross-attention partials, views on stream2 the second. A group of
@@ -1126,24 +1056,6 @@ static void dec_halves(Context* c, whisper_state* s, int gmax, bool xdirect, Dec
     a = DecView{0, 0, s->stream, w.splitk, half, w.xo, w.xml};
     b = DecView{0, 0, s->stream2, w.splitk + half, half, w.xo ? w.xo + xoff * H * d : nullptr,
                 w.xml ? w.xml + xoff * H * 2 : nullptr};
-}
-
-// the two row groups of a decode step: rows [0, na) on the state's stream, [na, n) on stream2
-static void dec_views(Context* c, whisper_state* s, int n_tok, bool xdirect, DecView& a, DecView& b) {
-    const int na = (n_tok + 1) / 2, nb = n_tok - na;
-    dec_halves(c, s, na, xdirect, a, b);
-    a.r0 = 0; a.n = na;
-    b.r0 = na; b.n = nb;
-}
-
-// WHISPER_MI355X_DEC_GRAPHS2=1: the two row groups as two separate hipGraphs launched on two streams
-// (two hardware queues), instead of two branches of one graph
-static bool dec_two_graphs() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_DEC_GRAPHS2");
-        return e && atoi(e) == 1;
-    }();
-    return on;
 }
 
 static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, bool rows_identity, bool xdirect) {
@@ -1186,7 +1098,7 @@ static void ensure_cross_cache(Context* c, whisper_state* s, const std::vector<i
     std::vector<int> stale;
     int need = 0;
     for (int sl : slots) need = std::max(need, sl + 1);
-    ensure_cross(c, w, need);
+    ensure_cross(c, s, need);
     for (int sl : slots)
         if (!w.cross_fresh[sl]) stale.push_back(sl);
     std::sort(stale.begin(), stale.end());
@@ -1512,11 +1424,6 @@ static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, st
     logits_finish(S, (int)act.size(), any, probs_rows);
 }
 
-static bool use_graphs() {
-    const char* e = getenv("WHISPER_MI355X_GRAPH");
-    return !(e && e[0] == '0');
-}
-
 // One decode step (decoder over n active clips + logits kernel) as a replayed hipGraph: the host
 // cost of ~11 launches per layer is paid once per distinct n at capture time.
 static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::vector<float>>& probs_rows) {
@@ -1525,48 +1432,12 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     const int n = (int)act.size();
     decoder_upload(c, s, n, n, false);
     const bool any = logits_prepare(S, act, false);
-    if (!use_graphs()) {
-        decoder_launch(c, s, n, n, true, s->direct);
-        logits_launch(c, s, n);
-        logits_finish(S, n, any, probs_rows);
-        return;
-    }
     whisper_state::DecGraph* G = nullptr;
+    const int sig = dec_path_sig();
     for (auto& g : s->dec_graphs)
-        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct) G = &g;
-    if (dec_two_graphs() && dec_groups(n) == 2 && cdiv(n, 2) <= 128 && s->ktime_mask == 0) {
-        // two graphs, one per row group and stream: both wait for the token upload, the logits kernel
-        // waits for both
-        DecView a, b;
-        dec_views(c, s, n, s->direct, a, b);
-        if (!G) {
-            whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, nullptr, {}};
-            hipGraph_t graph;
-            WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-            decoder_rows(c, s, a, a.n, true, s->direct, (double)a.n / n);
-            WM_CHECK(hipStreamEndCapture(s->stream, &graph));
-            WM_CHECK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
-            WM_CHECK(hipGraphDestroy(graph));
-            WM_CHECK(hipStreamBeginCapture(s->stream2, hipStreamCaptureModeThreadLocal));
-            decoder_rows(c, s, b, b.n, true, s->direct, (double)b.n / n);
-            WM_CHECK(hipStreamEndCapture(s->stream2, &graph));
-            WM_CHECK(hipGraphInstantiate(&g.exec2, graph, nullptr, nullptr, 0));
-            WM_CHECK(hipGraphDestroy(graph));
-            s->dec_graphs.push_back(std::move(g));
-            G = &s->dec_graphs.back();
-        }
-        WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
-        WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
-        WM_CHECK(hipGraphLaunch(G->exec2, s->stream2));
-        WM_CHECK(hipGraphLaunch(G->exec, s->stream));
-        WM_CHECK(hipEventRecord(s->ev_join, s->stream2));
-        WM_CHECK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
-        logits_launch(c, s, n);
-        logits_finish(S, n, any, probs_rows);
-        return;
-    }
+        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig) G = &g;
     if (!G) {
-        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, nullptr, {}};
+        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, nullptr, {}};
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
@@ -1584,40 +1455,48 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     kt_flush_graph(s, *G);
 }
 
-// Batches above WHISPER_MI355X_PAIR_MIN clips (default 128; 0 = off) run as two independent halves at
+// Batches above kPairMin clips run as two independent halves at
 // once: the first on this state, the second on a twin state (its own streams, workspace and decode
 // graphs, kept with this state for later calls) from a second host thread, and the twin's per-clip
 // results are appended. Each half is exactly a batch of its own clips (the same bits as two separate
 // calls), and one half's launch chain runs in the other's latency gaps: two 128-chunk large-v3 batches
 // in flight measured 3720 vs 3201 audio-s/s back to back (profiles/r03_overlap_two_batches.txt),
 // where one 256-row decode step ran as two lockstep row groups before.
-static int pair_min() {
-    const char* e = getenv("WHISPER_MI355X_PAIR_MIN");  // read per call
-    return e ? atoi(e) : 128;
-}
+static const int kPairMin = 128;
 
 static int full_batch_one(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                           int n_jobs, bool on_device, const FullOpts& o, bool single_api);
 
 int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                int n_jobs, bool on_device, const FullOpts& o, bool single_api) {
-    const int pm = pair_min();
-    if (single_api || pm <= 0 || n_jobs <= pm) return full_batch_one(c, s, p, pcm, n, n_jobs, on_device, o, single_api);
+    if (single_api || n_jobs <= kPairMin) return full_batch_one(c, s, p, pcm, n, n_jobs, on_device, o, single_api);
     WM_CHECK(hipSetDevice(c->device));
     if (!s->twin) s->twin = create_state(c);
     whisper_state* t = s->twin;
+    t->ktime_mask = s->ktime_mask;
     const int na = (n_jobs + 1) / 2;
     int ra = 0, rb = 0;
     std::exception_ptr ea, eb;
+    // the caller's abort callback need not be thread-safe: both halves reach it through one mutex
+    whisper_full_params pp = p;
+    struct AbortGate { std::mutex mu; ggml_abort_callback cb; void* ud; } gate{{}, p.abort_callback, p.abort_callback_user_data};
+    if (p.abort_callback) {
+        pp.abort_callback = [](void* u) -> bool {
+            AbortGate* g = (AbortGate*)u;
+            std::lock_guard<std::mutex> lk(g->mu);
+            return g->cb(g->ud);
+        };
+        pp.abort_callback_user_data = &gate;
+    }
     std::thread th([&] {
         try {
-            rb = full_batch_one(c, t, p, pcm + na, n + na, n_jobs - na, on_device, o, false);
+            rb = full_batch_one(c, t, pp, pcm + na, n + na, n_jobs - na, on_device, o, false);
         } catch (...) {
             eb = std::current_exception();
         }
     });
     try {
-        ra = full_batch_one(c, s, p, pcm, n, na, on_device, o, false);
+        ra = full_batch_one(c, s, pp, pcm, n, na, on_device, o, false);
     } catch (...) {
         ea = std::current_exception();
     }
@@ -1633,6 +1512,14 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
         s->decisions.push_back(std::move(t->decisions[j]));
     }
     s->decoded_tokens += t->decoded_tokens;
+    // the halves ran concurrently: a phase lasted as long as its slower half; kernel time adds up
+    for (int k = 0; k < 5; k++) s->phase_ms[k] = std::max(s->phase_ms[k], t->phase_ms[k]);
+    for (int k = 0; k < K_NCLASS; k++) {
+        s->kstat[k].ms += t->kstat[k].ms;
+        s->kstat[k].work += t->kstat[k].work;
+        s->kstat[k].count += t->kstat[k].count;
+        t->kstat[k] = KStat();
+    }
     return 0;
 }
 

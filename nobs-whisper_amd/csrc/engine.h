@@ -136,7 +136,6 @@ struct Workspace {
     void *mel_img = nullptr, *h1 = nullptr, *hn = nullptr, *qkv = nullptr, *att = nullptr, *ff = nullptr;
     float* x = nullptr;
     float* hs = nullptr;  // fp8 encoder: per-row scales of the quantized GEMM inputs
-    uint8_t* mxs = nullptr;  // fp8 encoder: E8M0 block scales of the FC1 output [rows][4d/32]
     // caches (cap_jobs slots). In direct mode `cross` is allocated on first use (prompts too long
     // for the direct prefill) and cross_fresh[slot] says whether a slot's cross K/V match enc.
     void *cross = nullptr, *self = nullptr;
@@ -215,8 +214,10 @@ struct whisper_state {
     struct KPending { int cls; hipEvent_t a, b; double work; };
     std::vector<KPending> kpending;
     std::vector<hipEvent_t> kpool;
-    // decode steps replayed as hipGraphs (one per active-sequence count and timing mask)
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; hipGraphExec_t exec; std::vector<KPending> ev; hipGraphExec_t exec2 = nullptr; };
+    // decode steps replayed as hipGraphs, one per (active-clip count, timing mask, cross form, path
+    // signature): `sig` encodes the per-call switches that pick the step's kernels (dec_path_sig), so a
+    // changed setting never replays a graph captured for another path
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step

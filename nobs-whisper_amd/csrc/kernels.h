@@ -43,8 +43,6 @@ enum Epi : int {
     EPI_CROSSKV = 5,   // T scatter into cross cache [slot][L][2][H][ctx][64]; K columns scaled
     EPI_QKV_DEC = 6,   // n<d: T q[m][n]*scale ; d<=n<2d: K cache (scaled) ; 2d<=n<3d: V cache
     EPI_GELU_F = 7,    // T out = tanh-GELU by formula in f32 (fp8 mode, and bf16 encoders: not ggml's f16 table)
-    EPI_GELU_MX = 8,   // fp8 mode: GELU by formula, then MX e4m3: out bytes [M][N] = e4m3(v / 2^e) with one
-                       // power-of-two scale per row and 32-column block, mx_scale[m][n/32] = e + 127 (E8M0)
 };
 
 // GGML block-quantized weight matrix [N][K] (the app's catalog ships q5_0 / q5_1
@@ -82,20 +80,16 @@ struct GemmArgs {
     const float* a_ln_w; const float* a_ln_b;
     // small-M decode GEMM: B given as GGML blocks (q.type != 0) instead of the compute type
     QMat q;
-    // decode-step split-K slabs stored write-through (sc1) instead of write-back
+    // decode-step split-K slabs stored write-through (sc1) instead of write-back (every decode step)
     int slab_wt;
-    // fp8 GEMM: EPI_GELU_MX writes the E8M0 block scales here; as an input (a_scale == null) they are
-    // the A operand's per-(row, 32-k block) scales, passed to the block-scaled MFMA
-    uint8_t* mx_scale;
     // decode-step GEMMs in fp8 mode: B is OCP e4m3 [N][K] bytes, column n scaled by w8_scale[n]
     const float* w8_scale;
 };
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
 // fp8 (OCP e4m3) operands with per-row f32 scales: C = (A8 . B8^T) * a_scale[m] * b_scale[n], then
-// the epilogue (EPI_STORE / EPI_GELU / EPI_GELU_F / EPI_GELU_MX / EPI_RESID); K % 128 == 0,
-// N % 16 == 0 (% 32 for EPI_GELU_MX). A/B strides in bytes. a_scale == null: A is MX-scaled, its
-// E8M0 block scales in a.mx_scale [M][K/32] (the output of an EPI_GELU_MX launch).
+// the epilogue (EPI_STORE / EPI_GELU / EPI_GELU_F / EPI_RESID); K % 128 == 0, N % 16 == 0. A/B strides
+// in bytes.
 void launch_gemm_fp8(DType dt, int epi, const GemmArgs& a, const float* a_scale, const float* b_scale, hipStream_t st);
 // q[r][:] = e4m3(x[r][:] / s[r]), s[r] = max|x[r][:]| / 448 (x in the MFMA type, K % 8 == 0)
 void launch_quant_rows_fp8(DType dt, const void* x, long rows, int K, void* q, float* s, hipStream_t st);
@@ -131,8 +125,8 @@ void launch_gemm_small(DType dt, int epi, const GemmArgs& a, bool lna, hipStream
 
 // ---- attention (kernels/attn.hip) --------------------------------------------------------------
 // encoder self-attention: qkv [B*T][3d] -> out [B*T][d]; softmax scale 1/sqrt(64)
-// variant: -1 = WHISPER_MI355X_ATTN (default 5), else 1 / 2 / 3 / 5 (attn_enc_kernel / _enc2_ / _enc3_ /
-// _enc2_ held to 128 VGPRs)
+// variant: -1 = the default (6: attn_enc2_kernel held to 128 VGPRs, scalar softmax FMAs), else
+// 1 / 2 / 3 / 5 (attn_enc_kernel / _enc2_ / _enc3_ / _enc2_ with packed FMAs; kernel benchmarks only)
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int T, int d, int H, hipStream_t st,
                          int variant = -1);
 // single-query attention for decoder tokens over a cache [slot][L][2][H][ctx][64]:
@@ -156,6 +150,9 @@ struct DecSlabs {
 // as the EPI_QKV_DEC epilogue); writes this position's k, v into the self cache at pos[i].
 void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int* slot, const int* pos, int n, int L,
                            int layer, int H, int ctx, int d, void* out, hipStream_t st);
+// decode steps of up to this many clips use the 1024-thread cache-form kernel (WHISPER_MI355X_XWIDE_MAX,
+// default 4, read per call)
+int attn_cross_wide_max();
 // cross attention of token i over n_kv[i] keys of the cross cache; q from the cross-Q slabs.
 void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
                             int L, int layer, int H, int ctx, int d, void* out, hipStream_t st);
@@ -171,13 +168,8 @@ bool xattn_supported(int d);
 int xattn_splits(int n, int Tn);
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st);
-// rev = 1: each split's 16-row tiles in reverse order (the engine alternates per decoder layer)
-// the same Q' from the cross-Q GEMM's split-K slabs (sl: q = (T)((sum_z slab + bias) * sl.scale), the
-// EPI_STORE reduce) in one launch: bit-identical to that reduce followed by launch_xattn_qproj
-void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
-                              hipStream_t st);
 void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
-                       float thr, float* opart, float* ml, hipStream_t st, int rev = 0);
+                       float thr, float* opart, float* ml, hipStream_t st);
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st);
 

@@ -1003,11 +1003,9 @@ void launch_attn_prefill(DType dt, const void* q, int q_stride, const void* cach
 
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st,
                          int variant_arg) {
-    static const int variant_env = [] {
-        const char* e = getenv("WHISPER_MI355X_ATTN");
-        return e ? atoi(e) : 6;
-    }();
-    const int variant = variant_arg >= 0 ? variant_arg : variant_env;
+    // variant 6 (attn_enc2_kernel, 128 VGPRs, scalar softmax FMAs) unless a kernel benchmark asks for
+    // another (whisper_mi355x_bench_attn_encoder)
+    const int variant = variant_arg >= 0 ? variant_arg : 6;
     if (variant == 3 && d == H * 64) {
         dim3 grid(cdiv(Tn, 256), H, B);
         if (dt == DType::F16) attn_enc3_kernel<half_t><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
@@ -1056,7 +1054,7 @@ void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache
 
 // WHISPER_MI355X_XWIDE_MAX (default 4, read per call): decode steps of up to this many clips use the
 // 1024-thread cache-form kernel
-static int cross_wide_max() {
+int attn_cross_wide_max() {
     const char* e = getenv("WHISPER_MI355X_XWIDE_MAX");
     return e ? atoi(e) : 4;
 }
@@ -1066,7 +1064,7 @@ void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, con
     if (n <= 0) return;
     if (ctx > 1536) WM_FAIL("attention context %d > 1536", ctx);
     dim3 grid(n, H);
-    if (n <= cross_wide_max()) {
+    if (n <= attn_cross_wide_max()) {
         if (dt == DType::F16)
             attn_cross_step_wide_kernel<half_t><<<grid, 1024, 0, st>>>(sl, (const half_t*)cache, slot, n_kv, L, layer, H, ctx, d, (half_t*)out);
         else
@@ -1084,15 +1082,9 @@ void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int*
     if (n <= 0) return;
     if (ctx > 448) WM_FAIL("self-attention context %d > 448", ctx);
     const int hpb = H % 4 == 0 ? 4 : H % 2 == 0 ? 2 : 1;
-    // non-temporal K/V reads with WHISPER_MI355X_SELF_NT=1 (A/B: 3048-3053 vs 3050-3057 audio-s/s
-    // with the default policy, so off)
-    static const bool nt = [] {
-        const char* e = getenv("WHISPER_MI355X_SELF_NT");
-        return e && atoi(e) != 0;
-    }();
-#define WM_SELF(TT, HB)                                                                                                     \
-    if (nt) attn_self_step_kernel<TT, HB, true><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out); \
-    else attn_self_step_kernel<TT, HB, false><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
+    // default-policy K/V reads (non-temporal measured 3048-3053 vs 3050-3057 audio-s/s, not kept)
+#define WM_SELF(TT, HB) \
+    attn_self_step_kernel<TT, HB, false><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
 #define WM_SELF_H(TT) \
     do { if (hpb == 4) WM_SELF(TT, 4); else if (hpb == 2) WM_SELF(TT, 2); else WM_SELF(TT, 1); } while (0)
     if (dt == DType::F16) WM_SELF_H(half_t);

@@ -795,29 +795,14 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ f32x4 mfma_mx8(i32x8 a, i32x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
-// A scale = byte SEL of `sp` (the opsel operand selects the byte: probed, tools/probe/mx_opsel.hip), so
-// four fragments' E8M0 scales travel in one VGPR
-template <int SEL>
-__device__ __forceinline__ f32x4 mfma_mx8s(i32x8 a, i32x8 b, f32x4 c, int sp) {
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, SEL, sp, 0, 127);
-}
-
-// MXA: A carries MX block scales (E8M0 per row and 32-k block, g.mx_scale [M][K/32], the output of an
-// EPI_GELU_MX launch) instead of a per-row f32 scale: each K-tile's 4 scale bytes per row are staged
-// next to the A tile (one 4-byte LDS-DMA per lane of the first half-wave of every wave, issued with
-// the A stage so the counted waits still cover it) and handed to the block-scaled MFMA per lane (a
-// lane's 32 k values are one block).
-template <typename T, int EPI, bool MXA = false>
+template <typename T, int EPI>
 __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const int tiles_n, const float* __restrict__ sa,
                                                         const float* __restrict__ sb) {
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int BM = 256, BK = 128;  // BK in fp8 elements = bytes
     // one __shared__ object only: a second one beside the LDS-DMA staging array makes hipcc wait
-    // vmcnt(0) before the first LDS read of every K-step (guide §5 "Projection GEMM" item 4(a)); the
-    // MX scales of a K-tile (256 rows x 4 bytes) sit after each buffer's A and B images
-    constexpr int SC16 = MXA ? BM / 4 : 0;  // u32x4 per buffer for the scales
-    __shared__ u32x4 lds[2][(BM + 256) * 8 + SC16];
-    auto lsc_ptr = [&](int buf) -> uint32_t* { return (uint32_t*)&lds[buf][(BM + 256) * 8]; };
+    // vmcnt(0) before the first LDS read of every K-step (guide §5 "Projection GEMM" item 4(a))
+    __shared__ u32x4 lds[2][(BM + 256) * 8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
@@ -838,9 +823,6 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
             const int n = min(n0 + r, g.N - 1);
             b_src[h][i] = B + (long)n * g.K + c * 16;
         }
-    // MX scales of rows m0 + wave*32 + (lane & 31): one u32 (4 blocks = one K-tile) per row
-    const uint8_t* sc_src = nullptr;
-    if constexpr (MXA) sc_src = g.mx_scale + (long)min(m0 + wave * 32 + (lane & 31), g.M - 1) * (g.K / 32);
     auto stage_a = [&](int kt) {
         u32x4* st = &lds[kt & 1][0];
 #pragma unroll
@@ -849,10 +831,6 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
             for (int i = 0; i < 2; i++)
                 __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
-        if constexpr (MXA) {
-            if (lane < 32)
-                __builtin_amdgcn_global_load_lds((const void*)(sc_src + kt * 4), (lds_ptr_t)(lsc_ptr(kt & 1) + wave * 32), 4, 0, 0);
-        }
     };
     auto stage_b = [&](int kt) {
         u32x4* st = &lds[kt & 1][BM * 8];
@@ -869,7 +847,6 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     i32x8 a0[4], a1[4], b0[2], b1[2];
-    int s0 = 0, s1 = 0;  // MXA: byte i = E8M0 of A fragment i (its row, this lane's 32-k block)
     // lane l's operand registers 0-3 / 4-7 hold k = 16(l>>4) + [0, 16) / 64 + 16(l>>4) + [0, 16) of the
     // K-tile (probed on gfx950: tools/probe/mx_layout.hip), so the 16-byte chunks (l>>4) and
     // (l>>4) + 4 of the row are loaded: instruction k == memory k, and a 32-k MX block (scale lane
@@ -879,36 +856,21 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
         const u32x4 x = img[row * 8 + (c0 ^ sw)], y = img[row * 8 + ((c0 + 4) ^ sw)];
         return (i32x8){(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
     };
-    auto read_a = [&](int buf, int mq, i32x8 (&af)[4], int& sp) {
-        if constexpr (MXA) sp = 0;
+    auto read_a = [&](int buf, int mq, i32x8 (&af)[4]) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int r = wm * 128 + (mq * 4 + i) * 16 + (lane & 15);
-            af[i] = frag(&lds[buf][0], r);
-            if constexpr (MXA) sp |= (int)(((lsc_ptr(buf)[r] >> (8 * (lane >> 4))) & 0xFF) << (8 * i));
-        }
+        for (int i = 0; i < 4; i++) af[i] = frag(&lds[buf][0], wm * 128 + (mq * 4 + i) * 16 + (lane & 15));
     };
     auto read_b = [&](int buf, int nq, i32x8 (&bf)[2]) {
 #pragma unroll
         for (int j = 0; j < 2; j++) bf[j] = frag(&lds[buf][BM * 8], wn * 64 + (nq * 2 + j) * 16 + (lane & 15));
     };
-    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2], int sp) {
+    auto mfma_q = [&](int mq, int nq, const i32x8 (&af)[4], const i32x8 (&bf)[2]) {
         asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
-        if constexpr (MXA) {
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
-                acc[mq * 4 + 0][nq * 2 + j] = mfma_mx8s<0>(af[0], bf[j], acc[mq * 4 + 0][nq * 2 + j], sp);
-                acc[mq * 4 + 1][nq * 2 + j] = mfma_mx8s<1>(af[1], bf[j], acc[mq * 4 + 1][nq * 2 + j], sp);
-                acc[mq * 4 + 2][nq * 2 + j] = mfma_mx8s<2>(af[2], bf[j], acc[mq * 4 + 2][nq * 2 + j], sp);
-                acc[mq * 4 + 3][nq * 2 + j] = mfma_mx8s<3>(af[3], bf[j], acc[mq * 4 + 3][nq * 2 + j], sp);
-            }
-        } else {
+        for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++) acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
-        }
+            for (int j = 0; j < 2; j++) acc[mq * 4 + i][nq * 2 + j] = mfma_mx8(af[i], bf[j], acc[mq * 4 + i][nq * 2 + j]);
         __builtin_amdgcn_s_setprio(0);
         asm volatile("s_barrier" ::: "memory");
     };
@@ -922,20 +884,20 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
         read_b(buf, 0, b0);
-        read_a(buf, 0, a0, s0);
+        read_a(buf, 0, a0);
         if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
-        mfma_q(0, 0, a0, b0, s0);
+        mfma_q(0, 0, a0, b0);
         read_b(buf, 1, b1);
-        mfma_q(0, 1, a0, b1, s0);
-        read_a(buf, 1, a1, s1);
-        mfma_q(1, 1, a1, b1, s1);
+        mfma_q(0, 1, a0, b1);
+        read_a(buf, 1, a1);
+        mfma_q(1, 1, a1, b1);
         if (kt + 2 < nk) {
             stage_b(kt + 2);
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        mfma_q(1, 0, a1, b0, s1);
+        mfma_q(1, 0, a1, b0);
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -973,51 +935,8 @@ __global__ void __launch_bounds__(512) gemm8p_mx_kernel(const GemmArgs g, const 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
-        if constexpr (EPI == EPI_GELU_MX) {
-            // lanes l, l^1 hold the two 16-column halves of one 32-column block of row m: every lane
-            // takes part in the DPP exchange (rows past M compute on clamped data, store nothing)
-            const float am = m < g.M ? (MXA ? 1.0f : sa[m]) : 0.0f;
-            float bv[16];
-            const int nbias = min(n, g.N - 16);  // N % 32 == 0: the 16 columns are in bounds
-#pragma unroll
-            for (int k = 0; k < 16; k += 4) {
-                const float4 b = g.bias ? *(const float4*)(g.bias + nbias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-                bv[k] = b.x; bv[k + 1] = b.y; bv[k + 2] = b.z; bv[k + 3] = b.w;
-            }
-            float amax = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                v[k] = gelu_formula((v[k] * am) * bs[k] + bv[k]);
-                amax = fmaxf(amax, fabsf(v[k]));
-            }
-            amax = fmaxf(amax, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, amax), 0xB1, 0xF, 0xF, false)));
-            // power-of-two scale 2^e with amax / 2^e <= 448 (e = ceil(log2(amax / 448)))
-            int e = 0;
-            if (amax > 0.0f) {
-                int ex;
-                const float fr = frexpf(amax / 448.0f, &ex);
-                e = fr == 0.5f ? ex - 1 : ex;
-                e = max(-127, min(127, e));
-            }
-            const float inv = ldexpf(1.0f, -e);
-            if (m < g.M && n + 16 <= g.N) {
-                uint32_t w[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    int p = 0;
-                    p = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * q] * inv, -448.f), 448.f),
-                                                        fminf(fmaxf(v[4 * q + 1] * inv, -448.f), 448.f), p, false);
-                    p = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4 * q + 2] * inv, -448.f), 448.f),
-                                                        fminf(fmaxf(v[4 * q + 3] * inv, -448.f), 448.f), p, true);
-                    w[q] = (uint32_t)p;
-                }
-                *(u32x4*)((uint8_t*)g.out + (long)m * g.ldo + n) = (u32x4){w[0], w[1], w[2], w[3]};
-                if ((lane & 1) == 0) g.mx_scale[(long)m * (g.N / 32) + n / 32] = (uint8_t)(e + 127);
-            }
-            continue;
-        }
         if (m < g.M && n < g.N) {
-            const float am = MXA ? 1.0f : sa[m];
+            const float am = sa[m];
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = (v[k] * am) * bs[k];
             epilogue16<EPI, T, LT>(g, m, n, v, ltab);
@@ -1685,46 +1604,16 @@ void launch_gemm_small(DType dt, int epi, const GemmArgs& g, bool lna, hipStream
 
 int g_dec_splits = 0;  // debug/tuning override of the decode-step split count (0 = heuristic)
 static int dec_splits_override() { return g_dec_splits; }
-// WHISPER_MI355X_DEC_GELU_SPLITS=k (tuning, read per call): the decode-step GELU GEMM (FC1) with at most
-// k splits (1 = unsplit, the GELU in the GEMM's epilogue and no reduce launch); 0/unset = dec_splits_for
-static int dec_gelu_splits() {
-    const char* e = getenv("WHISPER_MI355X_DEC_GELU_SPLITS");
-    return e ? std::max(0, atoi(e)) : 0;
-}
-// decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU; default), or
-// with WHISPER_MI355X_DEC_FILL=0 the smallest reaching >= 160; both with chunks of >= 2 K-tiles and
-// at most WHISPER_MI355X_DEC_MAXS (12) splits. Independent of M, so a row's sums never depend on the
-// batch. Large-v3: FC1 2 -> 3 splits, QKV 3 -> 4, N = d GEMMs 7 -> 10, FC2 8 -> 12; decode 844 -> 838
-// ms per step at 128 clips, 659 -> 654 at 64, 433 -> 413 at 16 (profiles/r02_dec_fill_ab.txt; the
-// 12-split cap alone: 837 -> 839 at 128 clips, 422 -> 413 at 16).
+// decode-step split count: the largest keeping the grid <= 256 workgroups (one per CU), with chunks
+// of >= 2 K-tiles and at most 12 splits. Independent of M, so a row's sums never depend on the batch.
+// Large-v3: FC1 3 splits, QKV 4, N = d GEMMs 10, FC2 12; against the round-2 rule (the smallest count
+// reaching >= 160 workgroups, <= 8 splits) decode 844 -> 838 ms per step at 128 clips, 659 -> 654 at 64,
+// 433 -> 413 at 16 (profiles/r02_dec_fill_ab.txt). Decode-step weights are read once per step by one
+// workgroup each: non-temporal LDS-DMA (aux = 2).
 static int dec_splits_for(int tiles, int nk) {
-    static const bool fill = [] {
-        const char* e = getenv("WHISPER_MI355X_DEC_FILL");
-        return !(e && atoi(e) == 0);
-    }();
-    static const int maxs = [] {
-        const char* e = getenv("WHISPER_MI355X_DEC_MAXS");
-        return e ? std::max(1, std::min(16, atoi(e))) : 12;
-    }();
     int splits = 1;
-    if (fill) {
-        while (tiles * (splits + 1) <= 256 && splits < maxs && (splits + 1) * 2 <= nk) splits++;
-    } else {
-        while (tiles * splits < 160 && splits < 8 && (splits + 1) * 2 <= nk) splits++;
-    }
+    while (tiles * (splits + 1) <= 256 && splits < 12 && (splits + 1) * 2 <= nk) splits++;
     return splits;
-}
-// decode-step weights are read once per step by one workgroup each: non-temporal LDS-DMA (aux = 2;
-// 3058-3070 vs 3053-3059 audio-s/s). With the grid filled to <= 256 workgroups the default policy
-// measured 4-8 ms per step faster in one A/B (BENCH_KTIME=0) but the next bench on another box put
-// the cross-attention step at 90.9 instead of 86.1 us (profiles/r02_dec_nt_ab.txt); not adopted
-// without a same-box confirmation. WHISPER_MI355X_DEC_NT=0 selects the default policy (A/B).
-static bool dec_weight_nt() {
-    static const bool on = [] {
-        const char* e = getenv("WHISPER_MI355X_DEC_NT");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
 }
 
 template <typename T>
@@ -1738,16 +1627,6 @@ static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st
     if (npt <= 4) splitk_reduce_resid_ln_kernel<T, 4><<<g.M, 256, 0, st>>>(g, splits);
     else if (npt <= 8) splitk_reduce_resid_ln_kernel<T, 8><<<g.M, 256, 0, st>>>(g, splits);
     else WM_FAIL("fused LN width %d > 2048", g.N);
-}
-
-// big-GEMM tile order: 0 = row-major over (m-tile, n-tile) after the XCD remap; > 0 = groups of this
-// many m-tiles (WHISPER_MI355X_GEMM_GM, tuning)
-static int gemm_group_m() {
-    static const int v = [] {
-        const char* e = getenv("WHISPER_MI355X_GEMM_GM");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
 }
 
 // the plain split-K reduce of a decode step: one thread per 4 columns (N % 4 == 0), 64-thread
@@ -1772,7 +1651,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int tn = cdiv(g.N, 256);
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
-        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, gemm_group_m());
+        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, 0);
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
@@ -1797,7 +1676,6 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int mch = cdiv(g.M, 128);
         int splits = dec_splits_for(tiles, nk);
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
-        if (EPI == EPI_GELU && dec_gelu_splits() > 0) splits = std::min(splits, dec_gelu_splits());
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
         // below wastes less of its tile (measured 23 vs 51 us at M = 16, N = 51866)
         const bool small_unsplit = splits == 1 && !fused_ln && g.M <= 64 && !g.w8_scale;
@@ -1807,13 +1685,11 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
                 if (g.w8_scale) gemm_dec_kernel<T, EPI, false, 2, true><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
-                else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, false, 2><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
-                else gemm_dec_kernel<T, EPI, false><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
+                else gemm_dec_kernel<T, EPI, false, 2><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
                 return;
             }
             if (g.w8_scale) gemm_dec_kernel<T, EPI, true, 2, true><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
-            else if (dec_weight_nt()) gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
-            else gemm_dec_kernel<T, EPI, true><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
+            else gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
             } else {
@@ -1893,8 +1769,7 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     splits = cdiv(g.K, kc);
     if ((long)splits * g.M * g.N > g.splitk_ws_elems) return 0;
     if (g.w8_scale) gemm_dec_kernel<T, EPI_STORE, true, 2, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
-    else if (dec_weight_nt()) gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
-    else gemm_dec_kernel<T, EPI_STORE, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    else gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
     return splits;
 }
 
@@ -1910,21 +1785,15 @@ static void launch_mx_t(int epi, const GemmArgs& g, const float* sa, const float
         case EPI_STORE: gemm8p_mx_kernel<T, EPI_STORE><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_GELU: gemm8p_mx_kernel<T, EPI_GELU><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         case EPI_GELU_F: gemm8p_mx_kernel<T, EPI_GELU_F><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
-        case EPI_GELU_MX: gemm8p_mx_kernel<T, EPI_GELU_MX><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
-        case EPI_RESID:
-            if (sa) gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb);
-            else gemm8p_mx_kernel<T, EPI_RESID, true><<<grid, 512, 0, st>>>(g, tn, sa, sb);
-            break;
+        case EPI_RESID: gemm8p_mx_kernel<T, EPI_RESID><<<grid, 512, 0, st>>>(g, tn, sa, sb); break;
         default: WM_FAIL("fp8 GEMM epilogue %d not supported", epi);
     }
 }
 
 void launch_gemm_fp8(DType dt, int epi, const GemmArgs& g, const float* a_scale, const float* b_scale, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0) return;
-    const bool mx_in = !a_scale && g.mx_scale && epi == EPI_RESID;
-    const bool mx_out = epi == EPI_GELU_MX;
-    if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || (!a_scale && !mx_in) || !b_scale ||
-        (mx_out && (g.N % 32 != 0 || !g.mx_scale || !a_scale)) || (mx_in && (g.a_rpb != g.M || g.a_rstride != g.K))) WM_FAIL("fp8 gemm shape not supported (N=%d K=%d)", g.N, g.K);
+    if (g.K % 128 != 0 || g.N % 16 != 0 || g.a_rpb <= 0 || g.o_rpb <= 0 || !a_scale || !b_scale)
+        WM_FAIL("fp8 gemm shape not supported (N=%d K=%d)", g.N, g.K);
     if (dt == DType::F16) launch_mx_t<half_t>(epi, g, a_scale, b_scale, st);
     else launch_mx_t<bf16_t>(epi, g, a_scale, b_scale, st);
 }

@@ -414,17 +414,14 @@ __global__ void __launch_bounds__(LT2) logits_combine_kernel(const float* __rest
     }
 }
 
-// WHISPER_MI355X_LOGITS_SPLIT_MAX (default 16, read per call): rows up to this count take the split form
-static int logits_split_max() {
-    const char* e = getenv("WHISPER_MI355X_LOGITS_SPLIT_MAX");
-    return e ? atoi(e) : 16;
-}
+// rows up to this count take the split form (16 chunk workgroups per row + a combine)
+static const int kLogitsSplitMax = 16;
 
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v, TokOut* out, float* probs,
                    void* rec, hipStream_t st) {
     if (n_seq <= 0) return;
     if (v.n_vocab > NPT * LT) WM_FAIL("vocabulary %d > %d", v.n_vocab, NPT * LT);
-    if (rec && n_seq <= logits_split_max() && v.n_vocab <= 14 * LT2 * KS) {
+    if (rec && n_seq <= kLogitsSplitMax && v.n_vocab <= 14 * LT2 * KS) {
         logits_part_kernel<<<dim3(KS, n_seq), LT2, 0, st>>>(logits, ld, ctl, v, (LogitRec*)rec);
         logits_combine_kernel<<<n_seq, LT2, 0, st>>>(logits, ld, ctl, v, (const LogitRec*)rec, out, probs);
         return;

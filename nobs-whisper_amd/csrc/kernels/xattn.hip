@@ -136,93 +136,13 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
         }
 }
 
-// Q' projection fused with the cross-Q GEMM's split-K reduce (decode steps): grid (H, cdiv(n, 16), 4),
-// 256 threads. The workgroup first reduces q_h for its 16 tokens from the slabs, exactly as
-// splitk_reduce_kernel<EPI_STORE> would (sum over splits in order from 0, + bias, * scale, rounded to
-// T; every split's piece loaded at once), into an LDS image; then wave w computes 80 columns of its
-// quarter of Q'_h (blockIdx.z) for the 16 tokens, every Wk_h^T fragment loaded before the first MFMA,
-// with the same MFMA operands and order as xattn_qproj_kernel (A = Wk_h^T rows, B = q_h, K = 64): the
-// outputs are bit-identical to the reduce + qproj pair, one launch and one round trip fewer. (The first
-// form, one workgroup per (head, 16 tokens) walking 320 columns per wave, chained 20 L2 round trips.)
-template <typename T>
-__global__ void __launch_bounds__(256) xattn_qproj_slabs_kernel(const DecSlabs sl, const T* __restrict__ wkt, int n, int d,
-                                                                int H, float scale, T* __restrict__ qx) {
-    typedef typename Frag<T>::type FT;
-    const int h = blockIdx.x, i0 = blockIdx.y * 16, cq = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    __shared__ __attribute__((aligned(16))) T qimg[16 * 64];
-    constexpr int MT = 5;  // 16-column tiles per wave (d <= 1280: d / 16 columns per quarter per wave)
-    const int cpw = d / 16, c0 = cq * (d / 4) + wave * cpw;  // this wave's columns (d % 256 == 0)
-    const int nmt = cpw / 16;
-    // Wk_h^T fragments of this wave's columns, in flight under the slab reduce
-    FT af[MT][2];
-#pragma unroll
-    for (int mt = 0; mt < MT; mt++) {
-        const int cr = c0 + mt * 16 + (lane & 15);
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++)
-            af[mt][ks] = mt < nmt ? __builtin_bit_cast(FT, *(const u32x4*)(wkt + ((long)h * d + cr) * 64 + ks * 32 + 8 * (lane >> 4)))
-                                  : af[0][0];
-    }
-    {
-        const int tk = tid >> 4, c = h * 64 + (tid & 15) * 4, i = i0 + tk;
-        T o[4] = {(T)0.0f, (T)0.0f, (T)0.0f, (T)0.0f};
-        if (i < n) {
-            const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            float4 w[16];
-#pragma unroll
-            for (int z = 0; z < 16; z++) w[z] = z < sl.splits ? *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c) : zero4;
-            float4 v = zero4;
-#pragma unroll
-            for (int z = 0; z < 16; z++)
-                if (z < sl.splits) { v.x += w[z].x; v.y += w[z].y; v.z += w[z].z; v.w += w[z].w; }
-            for (int z = 16; z < sl.splits; z++) {  // WHISPER_MI355X_DEC_SPLITS above 16 only
-                const float4 u = *(const float4*)(sl.ws + z * sl.zstride + (long)i * sl.ld + c);
-                v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
-            }
-            const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                float x = vv[k];
-                if (sl.bias) x = x + sl.bias[c + k];
-                o[k] = (T)(x * sl.scale);
-            }
-        }
-        *(uint2*)&qimg[tk * 64 + (tid & 15) * 4] = *(const uint2*)o;
-    }
-    __syncthreads();
-    FT bq[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ks++) bq[ks] = __builtin_bit_cast(FT, *(const u32x4*)&qimg[(lane & 15) * 64 + ks * 32 + 8 * (lane >> 4)]);
-    const int i = i0 + (lane & 15);
-#pragma unroll
-    for (int mt = 0; mt < MT; mt++) {
-        if (mt >= nmt) break;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[mt][ks], bq[ks], acc);
-        if (i >= n) continue;
-        const int c = c0 + mt * 16 + 4 * (lane >> 4);
-        T hi[4], lo[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float v = acc[r] * scale;
-            hi[r] = (T)v;
-            lo[r] = (T)(v - (float)hi[r]);
-        }
-        *(uint2*)(qx + ((long)i * 2 * H + h) * d + c) = *(const uint2*)hi;
-        *(uint2*)(qx + ((long)i * 2 * H + H + h) * d + c) = *(const uint2*)lo;
-    }
-}
-
 // ---- one pass over E per (clip, split) ------------------------------------------------------------
 // NW waves x CT column tiles of 32: d = NW*CT*32, H = d/64, NQ = ceil(2H/16) score column tiles.
 // AUX: cache-policy bits of the E loads (2 = non-temporal).
 template <typename T, int NW, int CT, int AUX>
 __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
                                                              const T* __restrict__ qx, int Tn, int splits, float thr,
-                                                             float* __restrict__ opart, float* __restrict__ ml, int rev,
-                                                             int wt, int keep) {
+                                                             float* __restrict__ opart, float* __restrict__ ml) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
@@ -282,23 +202,14 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         prow[k] = row;
         poff[k] = xphys(row, pc) * 8;
     }
-    // rev: the split's tiles in reverse order (odd decoder layers: the tiles a workgroup read last in
-    // the previous layer, the most recently used lines of the die-level cache, come first)
-    auto tile_of = [&](int t) { return tb + (rev ? ntile - 1 - t : t); };
     auto issue = [&](int t) {
-        const int row0 = tile_of(t) * 16;
+        const int row0 = (tb + t) * 16;
         u32x4* st = stg + (t % NS) * TILE;
 #pragma unroll
         for (int k = 0; k < CT; k++) {
             const int gr = min(row0 + prow[k], Tn - 1);
-            // keep: the first `keep` clips' E with the default policy (candidates to stay in the MALL
-            // from one decoder layer to the next), the rest with AUX
-            if (i < keep)
-                __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]),
-                                                 (lds_ptr_t)(st + (wave + k * NW) * 64), 16, 0, 0);
-            else
-                __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]),
-                                                 (lds_ptr_t)(st + (wave + k * NW) * 64), 16, 0, AUX);
+            __builtin_amdgcn_global_load_lds((const void*)(E + (long)gr * D + poff[k]),
+                                             (lds_ptr_t)(st + (wave + k * NW) * 64), 16, 0, AUX);
         }
     };
 
@@ -368,7 +279,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             for (int w = 0; w < NW; w++) {
                 sv += red[(w * 16 + r) * RSR + h];
             }
-            const float s2 = tile_of(t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
+            const float s2 = (tb + t) * 16 + r < Tn ? sv * LOG2E : -INFINITY;
             const float mx = max16(s2);
             float alpha = 1.0f;
             if (mx > m_run + thr) {  // first tile (m_run = -inf) or the max moved by more than thr
@@ -424,9 +335,8 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         }
     }
 
-    // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2]. wt: write-through (sc1) 16-byte
-    // stores, so the partials (26 MB per launch at 128 clips) leave the XCD's L2 as they are written
-    // instead of at the kernel boundary in front of the combine
+    // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2] (write-through stores of the
+    // partials measured no faster, not kept)
     const int h = lane & 31;
     if (h < H) {
         float* o = opart + (((long)i * splits + sp) * H + h) * D;
@@ -436,8 +346,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             for (int g = 0; g < 4; g++) {
                 const int c = cw + k * 32 + 8 * g + 4 * hh;
                 const f32x4 v = {oacc[k][4 * g], oacc[k][4 * g + 1], oacc[k][4 * g + 2], oacc[k][4 * g + 3]};
-                if (wt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(o + c), "v"(v) : "memory");
-                else *(f32x4*)(o + c) = v;
+                *(f32x4*)(o + c) = v;
             }
     }
     if (tid < 16 * H && (tid & 15) == 0) {
@@ -588,55 +497,24 @@ bool xattn_supported(int d) { return d == 384 || d == 512 || d == 768 || d == 10
 void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, int H, float scale, void* qx,
                         hipStream_t st) {
     if (n <= 0) return;
-    // tile per wave: WHISPER_MI355X_XQP_TILE = 24 (32 columns x 64 tokens, default: twice the workgroups of
-    // the round-2 shape), 44 (64 x 64, round 2), 42, 22 (read per call; the same bits for each). 24 vs 44:
-    // 64-clip shard 2340-2352 vs 2314-2330 audio-s/s, 128 clips neutral (profiles/r03_xcomb_tok_ab.txt)
-    const char* e = getenv("WHISPER_MI355X_XQP_TILE");
-    const int tile = e ? atoi(e) : 24;
-#define WM_XQP(MT_, NT_)                                                                                                     \
-    do {                                                                                                                     \
-        dim3 grid(cdiv(d, 64 * MT_), H, cdiv(n, 16 * NT_));                                                                  \
-        if (dt == DType::F16)                                                                                                \
-            xattn_qproj_kernel<half_t, MT_, NT_><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx); \
-        else                                                                                                                 \
-            xattn_qproj_kernel<bf16_t, MT_, NT_><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx); \
-    } while (0)
-    if (tile == 44) WM_XQP(4, 4);
-    else if (tile == 42) WM_XQP(4, 2);
-    else if (tile == 22) WM_XQP(2, 2);
-    else WM_XQP(2, 4);
-#undef WM_XQP
-}
-
-void launch_xattn_qproj_slabs(DType dt, const DecSlabs& sl, const void* wkt, int n, int d, int H, float scale, void* qx,
-                              hipStream_t st) {
-    if (n <= 0) return;
-    if (d % 256 || d > 1280 || sl.ld % 4) WM_FAIL("fused Q' projection: d %d", d);
-    dim3 grid(H, cdiv(n, 16), 4);
+    // tile per wave: 32 columns x 64 tokens (MT 2, NT 4): twice the workgroups of the round-2 shape
+    // (64 x 64; the same bits), 64-clip shard 2340-2352 vs 2314-2330 audio-s/s, 128 clips neutral
+    // (profiles/r03_xcomb_tok_ab.txt)
+    dim3 grid(cdiv(d, 64 * 2), H, cdiv(n, 16 * 4));
     if (dt == DType::F16)
-        xattn_qproj_slabs_kernel<half_t><<<grid, 256, 0, st>>>(sl, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
+        xattn_qproj_kernel<half_t, 2, 4><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
     else
-        xattn_qproj_slabs_kernel<bf16_t><<<grid, 256, 0, st>>>(sl, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
+        xattn_qproj_kernel<bf16_t, 2, 4><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
 }
 
 template <typename T>
 static void launch_step_t(const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits, float thr,
-                          float* opart, float* ml, int rev, hipStream_t st) {
+                          float* opart, float* ml, hipStream_t st) {
     dim3 grid(splits, n);
     // E is streamed once per launch (491 MB at batch 128: more than the MALL holds), so its LDS-DMA
     // loads are non-temporal (aux = 2): 86.6 vs 102.4 us per decode launch, 3075 vs 2921 audio-s/s.
-    // WHISPER_MI355X_XNT=0 restores the default cache policy (A/B).
-    static const int aux = getenv("WHISPER_MI355X_XNT") ? atoi(getenv("WHISPER_MI355X_XNT")) : 2;
-    // WHISPER_MI355X_XO_WT=1: write-through partial-O stores (A/B)
-    static const int wt = getenv("WHISPER_MI355X_XO_WT") ? atoi(getenv("WHISPER_MI355X_XO_WT")) : 0;
-    // WHISPER_MI355X_XKEEP=k: the first k clips' E loads use the default cache policy (A/B of MALL residency
-    // across decoder layers: k clips of large-v3 E are 3.84 MB each against a 256 MB MALL)
-    static const int keep = getenv("WHISPER_MI355X_XKEEP") ? atoi(getenv("WHISPER_MI355X_XKEEP")) : 0;
-#define WM_XSTEP(NW_, CT_)                                                                                                \
-    if (aux == 2)                                                                                                          \
-        xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt, keep); \
-    else                                                                                                                   \
-        xattn_step_kernel<T, NW_, CT_, 0><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, rev, wt, keep)
+#define WM_XSTEP(NW_, CT_) \
+    xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml)
     switch (d) {
         case 384: WM_XSTEP(4, 3); break;
         case 512: WM_XSTEP(8, 2); break;
@@ -649,33 +527,24 @@ static void launch_step_t(const void* enc, const int* slot, const void* qx, int 
 }
 
 void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* qx, int n, int Tn, int d, int splits,
-                       float thr, float* opart, float* ml, hipStream_t st, int rev) {
+                       float thr, float* opart, float* ml, hipStream_t st) {
     if (n <= 0) return;
     if (splits < 1 || splits > 16 || splits > (Tn + 15) / 16) WM_FAIL("bad split count %d", splits);
-    if (dt == DType::F16) launch_step_t<half_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, rev, st);
-    else launch_step_t<bf16_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, rev, st);
+    if (dt == DType::F16) launch_step_t<half_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
+    else launch_step_t<bf16_t>(enc, slot, qx, n, Tn, d, splits, thr, opart, ml, st);
 }
 
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st) {
     if (n <= 0) return;
     if (splits > 16 || d % 128 || d > 1280) WM_FAIL("combine shape not supported");
-    // tokens per workgroup: WHISPER_MI355X_XCOMB_TOK = 4 / 8 / 16 (read per call); every choice gives the
-    // same bits. Default: 8 (twice the round-2 grid).
-    const char* e = getenv("WHISPER_MI355X_XCOMB_TOK");
-    const int tok = e ? atoi(e) : 8;
-#define WM_XCOMB(TOK_)                                                                                                       \
-    do {                                                                                                                     \
-        dim3 grid(H, cdiv(n, TOK_));                                                                                         \
-        if (dt == DType::F16)                                                                                                \
-            xattn_combine_kernel<half_t, TOK_><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out); \
-        else                                                                                                                 \
-            xattn_combine_kernel<bf16_t, TOK_><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out); \
-    } while (0)
-    if (tok == 16) WM_XCOMB(16);
-    else if (tok == 4) WM_XCOMB(4);
-    else WM_XCOMB(8);
-#undef WM_XCOMB
+    // 8 tokens per workgroup: twice the round-2 grid (16; the same bits), 64-clip shard 2174-2190 ->
+    // 2318-2324 audio-s/s, neutral at 128 clips (profiles/r03_xcomb_tok_ab.txt)
+    dim3 grid(H, cdiv(n, 8));
+    if (dt == DType::F16)
+        xattn_combine_kernel<half_t, 8><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
+    else
+        xattn_combine_kernel<bf16_t, 8><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
 }
 
 }  // namespace wm

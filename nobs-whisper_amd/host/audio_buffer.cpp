@@ -7,8 +7,6 @@
 #include <cmath>
 #include <cstring>
 
-#include "whisper_engine.h"
-#include "whisper_mi355x.h"
 
 namespace nobs {
 
@@ -141,183 +139,9 @@ std::vector<std::vector<float>> split_at_silences_with_overlap(const std::vector
     return chunks;
 }
 
-// ---- StreamingSession ----------------------------------------------------------------------------
-
-StreamingSession::StreamingSession(const WhisperEngine* engine, uint32_t input_rate, int channels,
-                                   const char* language, const char* vocabulary, int device)
-    : engine_(engine), rate_(input_rate), channels_(channels < 1 ? 1 : channels), has_lang_(language != nullptr),
-      has_vocab_(vocabulary != nullptr && vocabulary[0] != '\0'), lang_(language ? language : ""),
-      vocab_(vocabulary ? vocabulary : ""), device_(device), buf_(input_rate) {
-    if (engine_ && engine_->is_loaded()) worker_ = std::thread([this] { worker(); });  // state.rs:537-561
-}
-
-StreamingSession::~StreamingSession() {
-    if (!stopped_) stop();
-}
-
-int StreamingSession::on_input(const float* data, size_t n) {
-    std::vector<float> chunk;
-    bool got;
-    {
-        std::lock_guard<std::mutex> g(buf_mu_);
-        if (channels_ > 1) {
-            // state.rs:590-594: per frame, the channel sum / channels, pushed one sample at a time.
-            // Sums start at -0.0 as Rust's `impl Sum for f32` does (sign of an all-zero frame).
-            for (size_t f = 0; f + (size_t)channels_ <= n; f += (size_t)channels_) {
-                float s = -0.0f;
-                for (int c = 0; c < channels_; c++) s = s + data[f + c];
-                const float mono = s / (float)channels_;
-                buf_.push_samples(&mono, 1);
-            }
-            const size_t rem = n % (size_t)channels_;  // a partial last frame: chunks() yields it too
-            if (rem) {
-                float s = -0.0f;
-                for (size_t c = 0; c < rem; c++) s = s + data[n - rem + c];
-                const float mono = s / (float)channels_;
-                buf_.push_samples(&mono, 1);
-            }
-        } else {
-            buf_.push_samples(data, n);
-        }
-        got = buf_.take_chunk_at_silence(&chunk) || buf_.take_forced_chunk(&chunk);  // state.rs:600-606
-    }
-    if (!got) return 0;
-    std::lock_guard<std::mutex> g(q_mu_);
-    dispatched_.push_back((int)chunk.size());
-    if (worker_.joinable() && !closed_) {
-        queue_.push_back(std::move(chunk));
-        q_cv_.notify_one();
-    }
-    return 1;
-}
-
-bool StreamingSession::resample(const std::vector<float>& in, uint32_t rate, std::vector<float>* out) const {
-    if (rate == kWhisperRate) {  // audio.rs:332-334
-        *out = in;
-        return true;
-    }
-    const int n_in = (int)in.size();
-    const int n_out = whisper_mi355x_resample_len(n_in, (int)rate);
-    if (n_out < 0) return false;
-    out->assign((size_t)n_out, 0.0f);
-    const float* src = in.data();
-    float* dst = out->data();
-    return whisper_mi355x_resample_chunk(device_, &src, &n_in, 1, (int)rate, false, &dst) == 0;
-}
-
-void StreamingSession::transcribe_into(const std::vector<float>& pcm, const char* prev,
-                                       std::vector<std::string>* res) {
-    std::string text, msg;
-    const auto r = engine_->transcribe(pcm.data(), pcm.size(), has_lang_ ? lang_.c_str() : nullptr,
-                                       has_vocab_ ? vocab_.c_str() : nullptr, prev, &text, &msg);
-    if (r != WhisperError::Ok) {
-        errors_++;  // logged and skipped (state.rs:157-159, 774-776, 788-790)
-        return;
-    }
-    if (!text.empty()) res->push_back(text);
-}
-
-void StreamingSession::worker() {  // state.rs:122-167
-    for (;;) {
-        std::vector<float> chunk;
-        {
-            std::unique_lock<std::mutex> g(q_mu_);
-            q_cv_.wait(g, [this] { return closed_ || !queue_.empty(); });
-            if (queue_.empty()) return;
-            chunk = std::move(queue_.front());
-            queue_.pop_front();
-        }
-        std::vector<float> pcm;
-        if (!resample(chunk, rate_, &pcm)) {
-            std::lock_guard<std::mutex> g(q_mu_);
-            errors_++;
-            continue;
-        }
-        std::vector<std::string> got;
-        transcribe_into(pcm, has_last_context_ ? last_context_.c_str() : nullptr, &got);
-        if (!got.empty()) {
-            last_context_ = got.back();
-            has_last_context_ = true;
-            std::lock_guard<std::mutex> g(q_mu_);
-            results_.push_back(got.back());
-        }
-    }
-}
-
-std::string StreamingSession::stop() {
-    if (stopped_) return std::string();
-    stopped_ = true;
-    {
-        std::lock_guard<std::mutex> g(q_mu_);  // state.rs:672-677: the chunk sender is dropped
-        closed_ = true;
-        q_cv_.notify_all();
-    }
-    if (worker_.joinable()) worker_.join();  // state.rs:712-721
-    std::vector<std::string> all;
-    {
-        std::lock_guard<std::mutex> g(q_mu_);
-        all = results_;
-    }
-    std::vector<float> rest;
-    {
-        std::lock_guard<std::mutex> g(buf_mu_);
-        rest = buf_.take();  // audio.rs:299-327 stop_recording (empty -> NotRecording -> None)
-    }
-    // state.rs:732-795 (without a model the resampled remainder is never used: not resampled here)
-    std::vector<float> pcm;
-    const bool model = engine_ && engine_->is_loaded();
-    const bool have = model && !rest.empty() && resample(rest, rate_, &pcm);
-    if (have && pcm.size() > 1600) {
-        if (pcm.size() > 30u * kWhisperRate) {
-            const float* p = pcm.data();
-            const int n = (int)pcm.size();
-            int count = 0;
-            std::vector<int> bnd(n / (int)(kWhisperRate / 50) + 1);
-            std::vector<int> b;
-            if (whisper_mi355x_find_silence_boundaries(device_, &p, &n, 1, (int)kWhisperRate, false, &count,
-                                                       bnd.data(), (int)bnd.size(), nullptr, nullptr, 0) == 0)
-                b.assign(bnd.begin(), bnd.begin() + std::min(count, (int)bnd.size()));
-            else
-                errors_++;
-            for (const auto& c : split_at_silences_with_overlap(pcm, b, kWhisperRate))
-                transcribe_into(c, all.empty() ? nullptr : all.back().c_str(), &all);
-        } else {
-            transcribe_into(pcm, all.empty() ? nullptr : all.back().c_str(), &all);
-        }
-    }
-    {
-        std::lock_guard<std::mutex> g(q_mu_);
-        results_ = all;
-    }
-    std::string joined;  // state.rs:798
-    for (size_t i = 0; i < all.size(); i++) {
-        if (i) joined += ' ';
-        joined += all[i];
-    }
-    return trim(joined);
-}
-
-std::vector<int> StreamingSession::dispatched_lengths() const {
-    std::lock_guard<std::mutex> g(q_mu_);
-    return dispatched_;
-}
-
-std::vector<std::string> StreamingSession::results() const {
-    std::lock_guard<std::mutex> g(q_mu_);
-    return results_;
-}
-
 }  // namespace nobs
 
 // ---- C ABI (what a Rust or Python caller binds) ---------------------------------------------------
-
-namespace {
-int copy_out(const std::string& s, char* out, int cap) {
-    if ((int)s.size() + 1 > cap) return -100;
-    memcpy(out, s.c_str(), s.size() + 1);
-    return (int)s.size();
-}
-}  // namespace
 
 #define NOBS_API extern "C" __attribute__((visibility("default")))
 
@@ -357,29 +181,4 @@ NOBS_API void nobs_audio_buffer_info(void* b, long* out, float* noise_floor) {
 }
 NOBS_API float nobs_calculate_rms(const float* x, long n) { return nobs::calculate_rms(x, (size_t)n); }
 
-NOBS_API void* nobs_stream_new(void* engine, unsigned input_rate, int channels, const char* language,
-                               const char* vocabulary, int device) {
-    if (input_rate < 50) return nullptr;
-    return new nobs::StreamingSession((const nobs::WhisperEngine*)engine, input_rate, channels, language, vocabulary,
-                                      device);
-}
-NOBS_API int nobs_stream_push(void* s, const float* data, long n) {
-    return ((nobs::StreamingSession*)s)->on_input(data, (size_t)n);
-}
-NOBS_API int nobs_stream_stop(void* s, char* out, int cap) {
-    return copy_out(((nobs::StreamingSession*)s)->stop(), out, cap);
-}
-// dispatched chunk lengths (input-rate samples); returns the count (only the first cap are written)
-NOBS_API int nobs_stream_dispatched(void* s, int* out, int cap) {
-    const auto d = ((nobs::StreamingSession*)s)->dispatched_lengths();
-    for (int i = 0; i < (int)d.size() && i < cap; i++) out[i] = d[i];
-    return (int)d.size();
-}
-NOBS_API int nobs_stream_n_results(void* s) { return (int)((nobs::StreamingSession*)s)->results().size(); }
-NOBS_API int nobs_stream_result(void* s, int i, char* out, int cap) {
-    const auto r = ((nobs::StreamingSession*)s)->results();
-    if (i < 0 || i >= (int)r.size()) return -1;
-    return copy_out(r[i], out, cap);
-}
-NOBS_API int nobs_stream_errors(void* s) { return ((nobs::StreamingSession*)s)->errors(); }
-NOBS_API void nobs_stream_free(void* s) { delete (nobs::StreamingSession*)s; }
+

@@ -1,9 +1,8 @@
-// C++ mirror of the reference's streaming capture path:
-//   * AudioBuffer      — src-tauri/src/audio.rs:29-241 (real-time VAD chunker with adaptive noise floor,
-//                        silence-split and forced-split chunk extraction, 200 ms overlap carry);
-//   * StreamingSession — src-tauri/src/state.rs:113-168 (transcription worker), 585-606 (the input
-//                        callback: stereo down-mix, push, dispatch a chunk) and 655-798 (stop: join the
-//                        worker, transcribe the remaining audio, split at silences above 30 s, join).
+// C++ mirror of the reference's capture-side chunker:
+//   * AudioBuffer — src-tauri/src/audio.rs:29-241 (real-time VAD chunker with adaptive noise floor,
+//                   silence-split and forced-split chunk extraction, 200 ms overlap carry).
+// The app's recording / worker / stop-thread machinery around it (state.rs) is UI state, out of scope
+// (SURVEY.md §2 row 4): it is not restated.
 //
 // The buffer runs on the host by design: it sees one capture callback (~10 ms of audio)
 // at a time, far below what a GPU launch pays off for. The chunks it dispatches are resampled and
@@ -13,18 +12,11 @@
 // Arithmetic follows the Rust source operation for operation in f32 (sequential sums, no contraction,
 // f32 constants), so chunk boundaries are identical to the app's for the same callback sequence.
 #pragma once
-#include <atomic>
-#include <condition_variable>
 #include <cstdint>
-#include <deque>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 namespace nobs {
-
-class WhisperEngine;
 
 // audio.rs:364-370 calculate_rms
 float calculate_rms(const float* x, size_t n);
@@ -62,50 +54,5 @@ class AudioBuffer {
 std::vector<std::vector<float>> split_at_silences_with_overlap(const std::vector<float>& audio,
                                                                const std::vector<int>& boundaries,
                                                                uint32_t sample_rate);
-
-class StreamingSession {
-  public:
-    // state.rs:515-558: buffer at the device rate, worker spawned when a model is loaded. language /
-    // vocabulary may be null (config "auto" / empty vocabulary).
-    StreamingSession(const WhisperEngine* engine, uint32_t input_rate, int channels, const char* language,
-                     const char* vocabulary, int device);
-    ~StreamingSession();
-
-    // state.rs:587-606, one input callback of interleaved frames. Returns 1 when it dispatched a chunk.
-    int on_input(const float* data, size_t n);
-    // state.rs:655-798 without the UI: the final combined text.
-    std::string stop();
-
-    std::vector<int> dispatched_lengths() const;  // samples at the input rate, in dispatch order
-    std::vector<std::string> results() const;     // the worker's non-empty texts, then the remaining audio's
-    int errors() const { return errors_; }
-
-  private:
-    void worker();
-    bool resample(const std::vector<float>& in, uint32_t rate, std::vector<float>* out) const;
-    void transcribe_into(const std::vector<float>& pcm16k, const char* prev, std::vector<std::string>* res);
-
-    const WhisperEngine* engine_;
-    uint32_t rate_;
-    int channels_;
-    bool has_lang_, has_vocab_;
-    std::string lang_, vocab_;
-    int device_;
-
-    std::mutex buf_mu_;  // the app's Arc<Mutex<AudioBuffer>>
-    AudioBuffer buf_;
-
-    mutable std::mutex q_mu_;  // the app's mpsc channel + results mutex
-    std::condition_variable q_cv_;
-    std::deque<std::vector<float>> queue_;
-    bool closed_ = false;
-    std::vector<int> dispatched_;
-    std::vector<std::string> results_;
-    std::string last_context_;
-    bool has_last_context_ = false;
-    std::atomic<int> errors_{0};
-    bool stopped_ = false;
-    std::thread worker_;
-};
 
 }  // namespace nobs

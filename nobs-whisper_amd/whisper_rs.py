@@ -434,15 +434,6 @@ def _stream_lib():
     L.nobs_audio_buffer_info.argtypes = [C.c_void_p, C.POINTER(C.c_long), fp]
     L.nobs_calculate_rms.restype = C.c_float
     L.nobs_calculate_rms.argtypes = [fp, C.c_long]
-    L.nobs_stream_new.restype = C.c_void_p
-    L.nobs_stream_new.argtypes = [C.c_void_p, C.c_uint, C.c_int, C.c_char_p, C.c_char_p, C.c_int]
-    L.nobs_stream_push.argtypes = [C.c_void_p, fp, C.c_long]
-    L.nobs_stream_stop.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
-    L.nobs_stream_dispatched.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
-    L.nobs_stream_n_results.argtypes = [C.c_void_p]
-    L.nobs_stream_result.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int]
-    L.nobs_stream_errors.argtypes = [C.c_void_p]
-    L.nobs_stream_free.argtypes = [C.c_void_p]
     return L
 
 
@@ -521,62 +512,6 @@ class AudioBuffer:
     def __del__(self):
         try:
             self.L.nobs_audio_buffer_free(self.ptr)
-        except Exception:
-            pass
-
-
-class StreamingSession:
-    """state.rs's streaming recording through the C++ mirror: on_input() is one capture callback
-    (state.rs:587-606: down-mix, push, dispatch a chunk to the worker, which resamples on the GPU and
-    transcribes with the previous text as context, state.rs:122-167); stop() is state.rs:655-798
-    (join the worker, transcribe the remaining audio, split above 30 s, join with spaces, trim)."""
-
-    def __init__(self, engine: "WhisperEngine", input_rate: int, channels: int = 1, language=None,
-                 vocabulary=None, device: int = 0):
-        self.L = _stream_lib()
-        enc = lambda s: s.encode() if s is not None else None  # noqa: E731
-        self.ptr = self.L.nobs_stream_new(engine.ptr if engine is not None else None, input_rate, channels,
-                                          enc(language), enc(vocabulary), device)
-        if not self.ptr:
-            raise ValueError(f"unsupported sample rate {input_rate}")
-        self.engine = engine
-
-    def on_input(self, data) -> int:
-        import numpy as np
-        a = np.ascontiguousarray(data, dtype=np.float32)
-        return self.L.nobs_stream_push(self.ptr, a.ctypes.data_as(C.POINTER(C.c_float)), len(a))
-
-    def stop(self) -> str:
-        buf = C.create_string_buffer(1 << 20)
-        n = self.L.nobs_stream_stop(self.ptr, buf, len(buf))
-        assert n >= 0, n
-        return buf.value.decode("utf-8", "replace")
-
-    def dispatched(self) -> list:
-        n = self.L.nobs_stream_dispatched(self.ptr, None, 0)
-        out = (C.c_int * max(1, n))()
-        self.L.nobs_stream_dispatched(self.ptr, out, n)
-        return list(out)[:n]
-
-    def results(self) -> list:
-        buf = C.create_string_buffer(1 << 20)
-        r = []
-        for i in range(self.L.nobs_stream_n_results(self.ptr)):
-            assert self.L.nobs_stream_result(self.ptr, i, buf, len(buf)) >= 0
-            r.append(buf.value.decode("utf-8", "replace"))
-        return r
-
-    def errors(self) -> int:
-        return self.L.nobs_stream_errors(self.ptr)
-
-    def close(self):
-        if self.ptr:
-            self.L.nobs_stream_free(self.ptr)
-            self.ptr = None
-
-    def __del__(self):
-        try:
-            self.close()
         except Exception:
             pass
 

@@ -373,19 +373,3 @@ class AudioBufferRef:
         chunk = self._emit(split)
         self.last_speech_pos = self.last_speech_pos - split if self.last_speech_pos > split else 0
         return chunk
-
-
-def stream_callback_ref(buf: AudioBufferRef, data, channels: int):
-    """state.rs:587-606 on the restated buffer: returns the dispatched chunk or None."""
-    data = np.asarray(data, dtype=np.float32)
-    if channels > 1:
-        for f in range(0, len(data), channels):
-            fr = data[f:f + channels]
-            s = np.cumsum(fr, dtype=np.float32)[-1]
-            buf.push_samples(np.array([_F(s) / _F(channels)], np.float32))
-    else:
-        buf.push_samples(data)
-    c = buf.take_chunk_at_silence()
-    if c is None:
-        c = buf.take_forced_chunk()
-    return c

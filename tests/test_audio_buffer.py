@@ -1,7 +1,6 @@
-"""The streaming VAD chunker (src-tauri/src/audio.rs:29-241 AudioBuffer) and the capture callback that
-drives it (state.rs:587-606), through the C++ mirror in nobs-whisper_amd/host/audio_buffer.cpp, against
-the numpy restatement in tests/oracle_py.py (AudioBufferRef). CPU only: the buffer runs on the host
-(DESIGN.md §0); the GPU side of streaming is tests/test_gpu_streaming.py.
+"""The streaming VAD chunker (src-tauri/src/audio.rs:29-241 AudioBuffer), through the C++ mirror in
+nobs-whisper_amd/host/audio_buffer.cpp, against the numpy restatement in tests/oracle_py.py
+(AudioBufferRef). CPU only: the buffer runs on the host.
 
 Bar: bit-exact. Every dispatched chunk (samples and length), the overlap carry, last_speech_pos, the
 noise floor and its frame count equal the restatement after every callback.
@@ -10,7 +9,7 @@ import numpy as np
 import pytest
 
 from make_model import synthetic_pcm
-from oracle_py import AudioBufferRef, rms_f32, stream_callback_ref
+from oracle_py import AudioBufferRef, rms_f32
 
 
 @pytest.fixture(scope="module")
@@ -105,31 +104,6 @@ def test_buffer_matches_restatement(wrs_host, sr, seconds, block, seed):
     rest_b, rest_r = b.take(), r.take()
     assert np.array_equal(rest_b, rest_r)
     assert _state(b) == _ref_state(r)
-
-
-def test_stereo_callbacks_match_restatement(wrs_host):
-    """state.rs:590-594: stereo frames are averaged and pushed one sample at a time (each a 1-sample
-    RMS window); the session without a model dispatches the same chunks as the restatement."""
-    sr = 16000
-    z = lambda sec: np.zeros(int(sec * sr), np.float32)  # noqa: E731
-    mono = np.concatenate([synthetic_pcm(1, 2.0, sr), z(1.0), synthetic_pcm(2, 1.5, sr), z(0.9),
-                           synthetic_pcm(3, 1.0, sr), z(0.3)]).astype(np.float32)
-    rng = np.random.default_rng(7)
-    stereo = np.stack([mono, (mono * np.float32(0.5) + rng.standard_normal(len(mono)).astype(np.float32)
-                              * np.float32(0.001))], axis=1).reshape(-1).astype(np.float32)
-    s = wrs_host.StreamingSession(None, sr, channels=2)
-    r = AudioBufferRef(sr)
-    exp = []
-    for off in range(0, len(stereo), 2 * 441):
-        blk = stereo[off:off + 2 * 441]
-        s.on_input(blk)
-        c = stream_callback_ref(r, blk, 2)
-        if c is not None:
-            exp.append(len(c))
-    assert s.dispatched() == exp
-    assert len(exp) >= 1
-    assert s.stop() == ""  # no model: nothing transcribed (state.rs:560 "streaming transcription disabled")
-    s.close()
 
 
 def test_unsupported_rate_is_an_error(wrs_host):

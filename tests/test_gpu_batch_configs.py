@@ -164,31 +164,3 @@ def test_largev3_bf16_b128_direct_vs_oracle(wrs, monkeypatch):
     st.close()
     ctx.close()
     print("bf16 b128 identical prefixes (clip, tokens, of):", prefixes)
-
-
-@pytest.mark.parametrize("name,a,b", [("XQ_FUSED", "0", "1"), ("XCOMB_TOK", "16", "8"), ("XCOMB_TOK", "16", "4"),
-                                         ("XQP_TILE", "44", "24"), ("XQP_TILE", "24", "42"), ("XQP_TILE", "24", "22")])
-def test_direct_form_switches_bit_identical(wrs, monkeypatch, name, a, b):
-    """Decode-step variants of the direct cross form that must not change a bit, on 48 large-v3 clips
-    (d = 1280, bf16; every token id, probability and timestamp): WHISPER_MI355X_XQ_FUSED=1 (the
-    cross-Q split-K reduce inside the Q' projection, xattn_qproj_slabs_kernel) == the reduce launch +
-    xattn_qproj_kernel; WHISPER_MI355X_XCOMB_TOK 16 vs 8 vs 4 tokens per xattn_combine_kernel workgroup;
-    WHISPER_MI355X_XQP_TILE, the Q' projection's tile per wave."""
-    from conftest import model_path
-    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
-    monkeypatch.setenv("WHISPER_MI355X_STATE_POOL", "0")  # fresh states: decode graphs captured per setting
-    path = model_path("large-v3-2L+conf")
-    clips = [synthetic_pcm(k % 24, seconds=30.0 - 0.5 * (k % 3)) for k in range(48)]
-    p = wrs.reference_full_params("en")
-    ctx = wrs.WhisperContext(path, dtype=wrs.BF16)
-    out = {}
-    for v in (a, b):
-        monkeypatch.setenv("WHISPER_MI355X_" + name, v)
-        st = ctx.create_state()
-        assert st.full_batch(p, clips) == 0
-        assert st.info()["direct"]
-        out[v] = ([seg_full(st.batch_segments(j)) for j in range(48)], [st.decisions(j) for j in range(48)])
-        st.close()
-    ctx.close()
-    assert out[a] == out[b]
-    assert sum(len(s) for s in out[a][0]) >= 48

@@ -163,80 +163,6 @@ def sys_path_tools():
         sys.path.insert(0, tools)
 
 
-# ---- MX hand-off FC1 -> FC2 (EPI_GELU_MX, then an MX-scaled A operand) ---------------------------------
-def _mx_fn(L):
-    f = L.whisper_mi355x_debug_gemm_fp8_mx
-    f.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                  C.c_int, C.c_void_p, C.c_void_p]
-    return f
-
-
-@pytest.mark.parametrize("M,N,K", [(300, 1280, 1280), (1500, 5120, 1280), (257, 1536, 384)])
-def test_gemm_fp8_gelu_mx_epilogue(wrs, ctx, M, N, K):
-    """FC1 with the MX epilogue: GELU(C) (C as in the per-row path) quantized to e4m3 with one
-    power-of-two scale 2^e per (row, 32-column block), e = ceil(log2(block amax / 448)): the decoded
-    values are within half an e4m3 step (at the value's binade, times 2^e) of GELU(C), and every
-    block's largest |q| lies in [224, 448] (a block amax just above 224 * 2^e may round to 224)."""
-    L = wrs.lib()
-    rng = np.random.default_rng(M + N + K)
-    ok = np.array([b for b in range(256) if not np.isnan(DEC[b])], np.uint8)
-    A8 = rng.choice(ok, (M, K)).astype(np.uint8)
-    B8 = rng.choice(ok, (N, K)).astype(np.uint8)
-    sa = rng.uniform(0.001, 0.01, M).astype(np.float32)
-    sb = (rng.uniform(0.0001, 0.001, N) * 0.1).astype(np.float32)
-    bias = rng.standard_normal(N).astype(np.float32)
-    q0, s0 = np.zeros((M, N), np.uint8), np.zeros((M, N // 32), np.uint8)
-    ptrs = [_dev(L, ctx, a) for a in (A8, sa, B8, sb, bias, q0, s0)]
-    pa, psa, pb, psb, pbias, pq, ps = ptrs
-    assert _mx_fn(L)(ctx.ptr, 8, C.c_void_p(pa), C.c_void_p(psa), C.c_void_p(ps), M, K, C.c_void_p(pb),
-                     C.c_void_p(psb), N, C.c_void_p(pbias), C.c_void_p(pq)) == 0
-    q, sc = _get(L, ctx, pq, q0), _get(L, ctx, ps, s0)
-    for p in ptrs:
-        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
-    a64, b64 = DEC[A8], DEC[B8]
-    pre = (a64 @ b64.T) * sa[:, None].astype(np.float64) * sb[None, :].astype(np.float64) + bias
-    mag = (np.abs(a64) @ np.abs(b64).T) * sa[:, None] * sb[None, :]
-    ref = 0.5 * pre * (1.0 + np.tanh(np.sqrt(2.0 / np.pi) * (pre + 0.044715 * pre ** 3)))
-    scale = 2.0 ** (sc.astype(np.float64) - 127.0)
-    full_scale = np.repeat(scale, 32, axis=1)
-    deq = DEC[q]
-    assert not np.isnan(deq).any()
-    blk = np.abs(deq).reshape(M, N // 32, 32).max(axis=2)
-    assert ((blk >= 224.0) | (blk == 0.0)).all() and (blk <= 448.0).all()
-    err = np.abs(deq * full_scale - ref)
-    bound = 0.5 * e4m3_spacing(deq) * full_scale + 1.13 * (1e-4 * mag + 1e-6) + 1e-6 * np.abs(ref)
-    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
-
-
-@pytest.mark.parametrize("M,N,K", [(300, 1280, 5120), (1500, 1280, 5120), (257, 384, 1536)])
-def test_gemm_fp8_mx_a_operand(wrs, ctx, M, N, K):
-    """FC2 with an MX-scaled A (per (row, 32-k block) E8M0 scales into the block-scaled MFMA):
-    x += (A8 * 2^(S - 127)) . B8^T * sb + bias, against float64 numpy of the same bytes."""
-    L = wrs.lib()
-    rng = np.random.default_rng(7 * M + N + K)
-    ok = np.array([b for b in range(256) if not np.isnan(DEC[b])], np.uint8)
-    A8 = rng.choice(ok, (M, K)).astype(np.uint8)
-    B8 = rng.choice(ok, (N, K)).astype(np.uint8)
-    S = rng.integers(118, 128, (M, K // 32)).astype(np.uint8)
-    sb = rng.uniform(0.0001, 0.001, N).astype(np.float32)
-    bias = rng.standard_normal(N).astype(np.float32)
-    x0 = rng.standard_normal((M, N)).astype(np.float32)
-    ptrs = [_dev(L, ctx, a) for a in (A8, S, B8, sb, bias, x0)]
-    pa, ps, pb, psb, pbias, px = ptrs
-    assert _mx_fn(L)(ctx.ptr, 2, C.c_void_p(pa), None, C.c_void_p(ps), M, K, C.c_void_p(pb), C.c_void_p(psb), N,
-                     C.c_void_p(pbias), C.c_void_p(px)) == 0
-    out = _get(L, ctx, px, x0).astype(np.float64)
-    for p in ptrs:
-        L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
-    a64 = DEC[A8] * np.repeat(2.0 ** (S.astype(np.float64) - 127.0), 32, axis=1)
-    b64 = DEC[B8]
-    ref = x0 + (a64 @ b64.T) * sb[None, :].astype(np.float64) + bias
-    mag = (np.abs(a64) @ np.abs(b64).T) * sb[None, :]
-    bound = 1e-4 * mag + 1e-6 + 1e-6 * np.abs(x0)
-    err = np.abs(out - ref)
-    assert (err <= bound).all(), f"max err {err.max()}, worst ratio {(err / bound).max()}"
-
-
 def _e4m3_table():
     """OCP e4m3fn decode of every byte (0x7f / 0xff are NaN)."""
     b = np.arange(256)
