@@ -117,10 +117,12 @@ def host_cpu() -> dict:
                 omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"))
 
 
-def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: int = 8) -> dict:
+def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: int = 0) -> dict:
     """The CPU oracle (restated whisper.cpp algorithm, C++/OpenMP) on a bounded sample of the same
-    workload: 1 chunk = mel + encoder + cross-KV + 3-token prefill + n_sample_tokens decode steps,
-    extrapolated to n_tokens decode steps per chunk."""
+    workload: 1 chunk = mel + encoder + cross-KV + 3-token prefill + n_sample_tokens decode steps
+    (default: all n_tokens of the fixed-work mode, so nothing is extrapolated; large-v3 on 16 threads
+    is ~13 s of encoder + ~4 s of decode)."""
+    n_sample_tokens = n_sample_tokens or n_tokens
     from make_model import synthetic_pcm
     from oracle_py import Oracle
     o = Oracle(model_path, mode=1, n_threads=threads)
@@ -144,11 +146,12 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
     per_step = (t4 - t3) / n_sample_tokens
     chunk_s = (t1 - t0) + (t2 - t1) + (t3 - t2) + n_tokens * per_step
     cpu = host_cpu()
+    extra = "" if n_sample_tokens == n_tokens else f", extrapolated to {n_tokens} steps/chunk"
     return dict(value=round(30.0 / chunk_s, 3), unit="audio-sec/s", cores=threads, kind="port",
                 host_cpu=cpu,
                 sample=(f"1 x 30 s chunk: mel {t1 - t0:.2f}s + encoder/cross-KV {t2 - t1:.2f}s + prefill {t3 - t2:.2f}s "
-                        f"+ {n_sample_tokens} decode steps ({per_step * 1e3:.0f} ms/step) measured, extrapolated to "
-                        f"{n_tokens} steps/chunk; oracle/ = restated whisper.cpp CPU algorithm (not whisper.cpp), "
+                        f"+ {n_sample_tokens} decode steps ({per_step * 1e3:.0f} ms/step) measured{extra}; "
+                        f"oracle/ = restated whisper.cpp CPU algorithm (not whisper.cpp), "
                         f"{threads} OpenMP threads = every CPU this job may use (affinity {cpu['affinity']}, "
                         f"cgroup cpu.max {cpu['cgroup_cpu_max']}) of a {cpu['logical_cpus']}-CPU {cpu['model']} host"))
 
@@ -156,7 +159,17 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
 # kernel symbol of each class in the rocprofv3 PMC output (tools/pmc.sh -> tools/pmc_traffic.py), per
 # cross-attention form for the decode-step class: straight from the encoder output, or the cached K/V
 K_SYMBOL = {("gemm_encoder", None): r"gemm8p_kernel", ("attn_encoder", None): r"attn_enc2_kernel",
-            ("attn_cross_decode", True): r"xattn_step_kernel", ("attn_cross_decode", False): r"attn_cross_step_kernel"}
+            ("attn_cross_decode", True): r"xattn_step_kernel",
+            ("attn_cross_decode", False): r"attn_cross_step_(wide_)?kernel"}
+
+
+def cross_step_grid(direct: bool, nb: int, heads: int, wide_max: int = 4) -> int:
+    """Threads per decode-step launch of the cross-attention kernel (the PMC pass is keyed by it):
+    direct form, xattn_step_kernel: xattn_splits(nb) x nb workgroups of 512 threads; cache form,
+    attn_cross_step_kernel: nb x H workgroups of 256 threads, or 1024 (the wide kernel) at <= 4 clips."""
+    if direct:
+        return max(1, min(16, -(-256 // nb))) * nb * 512
+    return nb * heads * (1024 if nb <= wide_max else 256)
 
 
 def pmc_traffic(kernel_class: str, direct: bool | None, grid_threads: int | None):
@@ -370,6 +383,8 @@ def main():
     ap.add_argument("--variant-steps", type=int, default=3)
     ap.add_argument("--inflight-line", type=int, default=1,
                     help="with --variants: also a serving line with two batches in flight (two states)")
+    ap.add_argument("--f16-line", type=int, default=1,
+                    help="with --dtype bf16: also time the same config with f16 weights (the token-exact path)")
     ap.add_argument("--fallback-line", type=int, default=0,
                     help="also time the reference's verbatim FullParams with temperature fallback (slow on "
                          "untrained weights: most windows fall back to sampled re-decodes)")
@@ -574,6 +589,56 @@ def main():
                                  ms_per_batch=round(1e3 * el / (2 * args.variant_steps), 2), batches_in_flight=2))
             st2.close()
 
+        # SURVEY.md §8d's clock from PCM on the host: the same step with the chunks handed over as host
+        # arrays (whisper_full's own boundary), so the 1.92 MB H2D copy per chunk is inside the timed
+        # region. Reported beside `value` (the contract's number has the inputs resident in HBM).
+        if nb:
+            host_pcm = [synthetic_pcm(cid) for cid in ids]
+
+            def step_host():
+                rc = st.full_batch(params, host_pcm, on_device=False, fixed_tokens=args.tokens)
+                assert rc == 0, rc
+            step_host()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(args.variant_steps):
+                step_host()
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.time() - t0, dist, "cuda")
+            variants.append(dict(workload="PCM on the host (PCIe-inclusive: H2D copy of every chunk inside the step), "
+                                          "language en, no prompt",
+                                 value=round(30.0 * global_batch * args.variant_steps / el, 2),
+                                 ms_per_step=round(1e3 * el / args.variant_steps, 2), pcie_inclusive=True))
+            del host_pcm
+
+    # the f16 engine on the same config: whisper.cpp's own weight type, the token-exact parity path
+    # (tests/test_gpu_fulldepth.py); bf16 is the headline dtype BASELINE names. One GPU only.
+    if args.f16_line and args.dtype == "bf16" and nb and world == 1:
+        ctx16 = wrs.WhisperContext(model_path, dtype=wrs.F16, gpu_device=local_rank)
+        st16 = ctx16.create_state()
+
+        def step16():
+            rc = st16.full_batch(params, jobs, on_device=True, fixed_tokens=args.tokens)
+            assert rc == 0, rc
+        step16()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(args.variant_steps):
+            step16()
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.time() - t0, dist, "cuda")
+        variants.append(dict(workload="f16 weights (the GGML file's own type; token-exact against the oracle), "
+                                      "same chunks and fixed-work decode, language en, no prompt", dtype="f16",
+                             value=round(30.0 * global_batch * args.variant_steps / el, 2),
+                             ms_per_step=round(1e3 * el / args.variant_steps, 2),
+                             phase_ms_last_step={k: round(v, 1) for k, v in st16.phase_ms().items()}))
+        st16.close()
+        ctx16.close()
+
     frontend = None
     if args.frontend and rank == 0 and nb:
         frontend = bench_frontend(wrs, ctx, buf, nb, n)
@@ -593,9 +658,9 @@ def main():
             roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None)
         grid = None
-        if K_NAMES[dom] == "attn_cross_decode" and form["direct"]:
-            # decode-step launches of xattn_step_kernel: splits x clips workgroups of 512 threads
-            grid = max(1, min(16, -(-256 // nb))) * nb * 512
+        if K_NAMES[dom] == "attn_cross_decode":
+            from make_model import SHAPES
+            grid = cross_step_grid(bool(form["direct"]), nb, SHAPES[args.model][3])
         traffic, src = pmc_traffic(K_NAMES[dom], form["direct"], grid)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

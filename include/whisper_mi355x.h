@@ -48,6 +48,15 @@ WHISPER_API int whisper_mi355x_broadcast_weights(struct whisper_context * ctx, c
 WHISPER_API int whisper_mi355x_full_batch(struct whisper_context * ctx, struct whisper_state * state,
                                           struct whisper_full_params params, const float * const * pcm,
                                           const int * n_samples, int n_jobs, bool pcm_on_device, int fixed_tokens);
+/* Parity-test hook: the fixed-work batch with teacher forcing. The token decoded after step i of job j
+ * is forced[j * fixed_tokens + i] (whatever the logits rules chose), and the raw logits of the jobs
+ * spot[0..n_spot) at every step i (step 0 = the prefill) go to spot_logits[(i * n_spot + k) * n_vocab]
+ * (host memory, fixed_tokens * n_spot * n_vocab floats). The kernels are the ones whisper_mi355x_full_batch
+ * runs on the same batch. n_jobs <= 128. */
+WHISPER_API int whisper_mi355x_full_batch_forced(struct whisper_context * ctx, struct whisper_state * state,
+                                                 struct whisper_full_params params, const float * const * pcm,
+                                                 const int * n_samples, int n_jobs, bool pcm_on_device, int fixed_tokens,
+                                                 const int * forced, const int * spot, int n_spot, float * spot_logits);
 WHISPER_API int whisper_mi355x_batch_n_segments(struct whisper_state * state, int job);
 WHISPER_API const char * whisper_mi355x_batch_segment_text(struct whisper_state * state, int job, int i_segment);
 WHISPER_API int64_t whisper_mi355x_batch_segment_t0(struct whisper_state * state, int job, int i_segment);

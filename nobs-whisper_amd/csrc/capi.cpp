@@ -452,6 +452,21 @@ int whisper_mi355x_full_batch(struct whisper_context* ctx, struct whisper_state*
     o.fixed_tokens = fixed_tokens;
     return guarded(s, [&] { return full_batch(&ctx->c, s, p, pcm, n, n_jobs, on_device, o, false); });
 }
+int whisper_mi355x_full_batch_forced(struct whisper_context* ctx, struct whisper_state* s, struct whisper_full_params p,
+                                     const float* const* pcm, const int* n, int n_jobs, bool on_device, int fixed_tokens,
+                                     const int* forced, const int* spot, int n_spot, float* spot_logits) {
+    if (!ctx || !s || n_jobs <= 0 || fixed_tokens <= 0 || !forced || n_spot < 0 || (n_spot && (!spot || !spot_logits)))
+        return -1;
+    for (int k = 0; k < n_spot; k++)
+        if (spot[k] < 0 || spot[k] >= n_jobs) return -1;
+    FullOpts o;
+    o.fixed_tokens = fixed_tokens;
+    o.forced = forced;
+    o.spot = spot;
+    o.n_spot = n_spot;
+    o.spot_logits = spot_logits;
+    return guarded(s, [&] { return full_batch(&ctx->c, s, p, pcm, n, n_jobs, on_device, o, false); });
+}
 int whisper_mi355x_batch_n_segments(struct whisper_state* s, int job) {
     return s && job >= 0 && job < (int)s->results.size() ? (int)s->results[job].size() : 0;
 }

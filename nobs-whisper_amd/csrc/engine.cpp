@@ -1324,6 +1324,23 @@ static void attempt_done(Sched& S, Job& j) {
     finish_window(S, j);
 }
 
+// teacher-forcing hook (FullOpts::spot): the raw logits rows of the spot jobs among `act` (row r of
+// w.logits belongs to act[r]) for step `step` of each
+static void copy_spot_logits(Sched& S, const std::vector<int>& act) {
+    if (!S.o.spot_logits || S.o.n_spot <= 0) return;
+    Workspace& w = S.s->ws;
+    const size_t V = S.c->hp.n_vocab;
+    for (int r = 0; r < (int)act.size(); r++)
+        for (int k = 0; k < S.o.n_spot; k++)
+            if (S.o.spot[k] == act[r]) {
+                const int step = S.jobs[act[r]].step;
+                if (step < 0 || step >= S.o.fixed_tokens) continue;
+                WM_CHECK(hipMemcpyAsync(S.o.spot_logits + ((size_t)step * S.o.n_spot + k) * V, w.logits + (size_t)r * V,
+                                        V * 4, hipMemcpyDeviceToHost, S.s->stream));
+            }
+    WM_CHECK(hipStreamSynchronize(S.s->stream));
+}
+
 // one whisper_full "sample + update" iteration for token index j.step; returns true if decoding continues
 static bool process_step(Sched& S, Job& j, const TokOut& r, const float* probs_row) {
     const Vocab& v = S.c->vocab;
@@ -1343,6 +1360,7 @@ static bool process_step(Sched& S, Job& j, const TokOut& r, const float* probs_r
         if (td.id >= v.token_beg) { td.tid = td.id; td.pt = td.p; }
         else { td.tid = r.tid; td.pt = r.pt; }
     }
+    if (S.o.forced && S.o.fixed_tokens > 0) td.id = S.o.forced[(long)j.slot * S.o.fixed_tokens + i];
     j.tokens.push_back(td);
     j.sum_logprobs_all += td.plog;
     S.decoded++;
@@ -1705,6 +1723,7 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
                 decoder_forward(c, s, nt, (int)act.size());
                 run_logits(S, act, true, probs_rows);
                 S.t_prefill += now_ms() - tp;
+                copy_spot_logits(S, act);
                 for (int r = 0; r < (int)act.size(); r++) {
                     Job& j = S.jobs[act[r]];
                     j.no_speech_prob = w.h_tout[r].nosp_prob;
@@ -1731,9 +1750,10 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
                 }
                 decode_step(S, act, probs_rows);
                 S.t_decode += now_ms() - td;
+                for (int r = 0; r < na; r++) S.jobs[act[r]].step++;
+                copy_spot_logits(S, act);
                 for (int r = 0; r < na; r++) {
                     Job& j = S.jobs[act[r]];
-                    j.step++;
                     if (!process_step(S, j, w.h_tout[r], probs_rows[r].empty() ? nullptr : probs_rows[r].data())) attempt_done(S, j);
                 }
             }

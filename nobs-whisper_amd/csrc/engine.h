@@ -242,6 +242,14 @@ void orphan_states(Context* c);
 
 struct FullOpts {
     int fixed_tokens = 0;
+    // teacher forcing (fixed-work mode only; a parity-test hook): the token chosen at step i of job j is
+    // replaced by forced[j * fixed_tokens + i] after the logits rules ran, so every later step decodes
+    // the given sequence through the same kernels; the raw logits of jobs spot[0..n_spot) are copied
+    // to spot_logits[(i * n_spot + k) * n_vocab] at every step i (prefill = step 0)
+    const int* forced = nullptr;
+    const int* spot = nullptr;
+    int n_spot = 0;
+    float* spot_logits = nullptr;
 };
 // whisper_full over n_jobs clips. B=1 with the state's own prompt_past/rng reproduces
 // whisper_full_with_state; B>1 treats every clip as a fresh state.

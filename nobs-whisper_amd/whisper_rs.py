@@ -145,6 +145,8 @@ def lib() -> C.CDLL:
         "whisper_lang_id": (C.c_int, [C.c_char_p]),
         "whisper_lang_str": (C.c_char_p, [C.c_int]),
         "whisper_mi355x_full_batch": (C.c_int, [vp, vp, FullParams, C.POINTER(vp), ip, C.c_int, C.c_bool, C.c_int]),
+        "whisper_mi355x_full_batch_forced": (C.c_int, [vp, vp, FullParams, C.POINTER(vp), ip, C.c_int, C.c_bool, C.c_int,
+                                                       ip, ip, C.c_int, C.POINTER(C.c_float)]),
         "whisper_mi355x_batch_n_segments": (C.c_int, [vp, C.c_int]),
         "whisper_mi355x_batch_segment_text": (C.c_char_p, [vp, C.c_int, C.c_int]),
         "whisper_mi355x_batch_segment_t0": (C.c_int64, [vp, C.c_int, C.c_int]),
@@ -311,6 +313,32 @@ class WhisperState:
                 ptrs[i] = a.ctypes.data
                 lens[i] = len(a)
         return self.L.whisper_mi355x_full_batch(self.ctx.ptr, self.ptr, params, ptrs, lens, n, on_device, fixed_tokens)
+
+    def full_batch_forced(self, params: FullParams, pcm_list, fixed_tokens: int, forced, spot, n_vocab: int,
+                          on_device: bool = False):
+        """whisper_mi355x_full_batch_forced: forced [n_jobs][fixed_tokens] token ids; returns (rc, logits
+        [fixed_tokens][len(spot)][n_vocab]) of the spot jobs at every step."""
+        import numpy as np
+        n = len(pcm_list)
+        ptrs = (C.c_void_p * n)()
+        lens = (C.c_int * n)()
+        keep = []
+        for i, x in enumerate(pcm_list):
+            if on_device:
+                ptrs[i], lens[i] = x[0], x[1]
+            else:
+                a = np.ascontiguousarray(x, dtype=np.float32)
+                keep.append(a)
+                ptrs[i] = a.ctypes.data
+                lens[i] = len(a)
+        f = np.ascontiguousarray(forced, dtype=np.int32).reshape(n, fixed_tokens)
+        sp = np.ascontiguousarray(spot, dtype=np.int32)
+        out = np.zeros((fixed_tokens, len(sp), n_vocab), np.float32)
+        ip_ = C.POINTER(C.c_int)
+        rc = self.L.whisper_mi355x_full_batch_forced(self.ctx.ptr, self.ptr, params, ptrs, lens, n, on_device, fixed_tokens,
+                                                     f.ctypes.data_as(ip_), sp.ctypes.data_as(ip_), len(sp),
+                                                     out.ctypes.data_as(C.POINTER(C.c_float)))
+        return rc, out
 
     def batch_segments(self, job: int) -> list:
         L = self.L
