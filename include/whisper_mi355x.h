@@ -123,6 +123,10 @@ WHISPER_API int whisper_mi355x_debug_gemm_small(struct whisper_context * ctx, in
                                                 const void * B, int N, const float * bias, void * out,
                                                 const float * ln_w, const float * ln_b, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
+/* Test hook: a persistent decode step's waits give up after this many 100 MHz ticks (default 5,000,000 =
+ * 50 ms); 0 makes every persistent launch give up, so each step takes the re-run path. Captured graphs
+ * keep the value they were captured with. */
+WHISPER_API void whisper_mi355x_set_pdec_spin(long ticks);
 /* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
  * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */
 // fp8 (OCP e4m3) GEMM with per-row f32 scales (A per row m, B per row n), then epilogue `epi`;

@@ -291,7 +291,8 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd); dfree(w.pd_sync);
+    if (w.h_pd_err) hipHostFree(w.h_pd_err);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
     if (w.h_tout) hipHostFree(w.h_tout);
@@ -788,9 +789,104 @@ static int quant_small_max() {
     return e ? atoi(e) : 32;
 }
 
+// The persistent decode step (kernels/pdec.hip) for decode steps of up to this many clips in the cache
+// form: WHISPER_MI355X_PDEC (default 4 = kPdecMaxRows; 0 = off; read per call).
+static int pdec_max() {
+    const char* e = getenv("WHISPER_MI355X_PDEC");
+    return e ? std::max(0, std::min(kPdecMaxRows, atoi(e))) : kPdecMaxRows;
+}
+
 // The per-call switches that choose a decode step's kernels, folded into the key of its captured graph.
 static int dec_path_sig() {
-    return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) | (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16);
+    return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) |
+           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26);
+}
+
+// A decode step of n clips runs as one persistent launch when the model shape has a kernel, the
+// weights are plain f16 / bf16 (not blocks, not the fp8 decoder copies), the device has the 256 CUs
+// the grid is built for, and the step is in the cross K/V cache form.
+static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
+    if (xdirect || s->pdec_block || n < 1 || n > pdec_max() || c->quant) return false;
+    if (c->fp8_enc && !c->dec8.empty()) return false;
+    if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head)) return false;
+    static const int cus = [] {
+        int dev = 0, v = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+        return v;
+    }();
+    return cus == 256;
+}
+
+// Device array of the decoder layers' pointers (once per context)
+static const PdecLayer* pdec_layers(Context* c) {
+    std::lock_guard<std::mutex> lk(c->pdec_mu);
+    if (!c->pdec_layers) {
+        std::vector<PdecLayer> h(c->hp.n_text_layer);
+        for (int l = 0; l < c->hp.n_text_layer; l++) {
+            const LayerW& L = c->w.dec[l];
+            h[l] = PdecLayer{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2, L.bqkv, L.bo, L.bxq, L.bxo, L.b1, L.b2,
+                             L.ln1_w, L.ln1_b, L.lnx_w, L.lnx_b, L.ln2_w, L.ln2_b};
+        }
+        void* p = nullptr;
+        WM_CHECK(hipMalloc(&p, h.size() * sizeof(PdecLayer)));
+        WM_CHECK(hipMemcpy(p, h.data(), h.size() * sizeof(PdecLayer), hipMemcpyHostToDevice));
+        c->pdec_layers = p;
+    }
+    return (const PdecLayer*)c->pdec_layers;
+}
+
+// One decode step of the view's rows as the persistent launch + the logits GEMM (graph-capturable).
+// The launch's error word is copied to the host (a node of the step's graph): decode_step checks it
+// after the step's synchronisation and re-runs the step on the per-kernel path if the launch gave up.
+static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab;
+    const int n = v.n;
+    hipStream_t st = v.st;
+    const size_t pd_floats = (size_t)kPdecMaxRows * 10 * d + 2 * 256 * 68;
+    if (!w.pd) {
+        dalloc(w.pd, pd_floats * sizeof(float));
+        dalloc(w.pd_sync, pdec_sync_bytes(L));
+        WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
+        *w.h_pd_err = 0;
+    }
+    PdecArgs a{};
+    a.layers = pdec_layers(c);
+    a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.n_audio_ctx = hp.n_audio_ctx;
+    a.tok_emb = c->w.tok_emb_f32 ? (const void*)c->w.tok_emb_f32 : c->w.tok_emb;
+    a.te_f32 = c->w.tok_emb_f32 != nullptr;
+    a.pos_d = c->w.pos_d;
+    a.lnd_w = c->w.lnd_w; a.lnd_b = c->w.lnd_b;
+    a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
+    a.self_cache = w.self; a.cross_cache = w.cross;
+    a.k_scale = c->k_scale;
+    float* p = w.pd;
+    const size_t R = kPdecMaxRows;
+    a.x0 = p; p += R * d;
+    a.x1 = p; p += R * d;
+    a.x2 = p; p += R * d;
+    a.qkv = p; p += R * 3 * d;
+    a.qx = p; p += R * d;
+    a.ff = p; p += R * 4 * d;
+    a.spart = p; p += 256 * 68;
+    a.xpart = p;
+    a.s_self = pdec_splits(n, H, hp.n_text_ctx);
+    a.s_cross = pdec_splits(n, H, hp.n_audio_ctx);
+    a.sync = w.pd_sync;
+    a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
+    a.gelu_tab = gelu_table_device();
+    a.spin_ticks = g_pdec_spin_ticks;
+    {
+        // weights once + cross K/V + self K/V of every row, per launch
+        const double bytes = 14.0 * d * d * 2 * L + (double)n * L * 2 * hp.n_audio_ctx * d * 2 + s->cur_self_work;
+        KT kt(s, K_PDEC, bytes, st);
+        launch_pdec(c->dt, a, st);
+    }
+    WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + pdec_err_offset(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
+    tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }
 
 // Decode step over <= 32 rows (the app's one clip per call, whisper.rs:83-85 / state.rs:147; one
@@ -932,6 +1028,19 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         gemm(KCLS, EPI_RESID, g);
         if (!fused && lnw) launch_layernorm(dt, dx, nullptr, n_tok, d, lnw, lnb, dh, st);
     };
+    // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
+    // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
+    const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
+    if (fused && pdec_use(c, s, n_tok, xdirect)) {
+        decoder_rows_pdec(c, s, v);
+        return;
+    }
+    // (the persistent and small-M paths embed the tokens themselves)
+    if (fused && !w8 && ((c->quant && n_tok <= quant_small_max()) || n_tok <= small_m_max()) && gemm_small_ok(n_tok, d, true) &&
+        gemm_small_ok(n_tok, 4 * d, false)) {
+        decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
+        return;
+    }
     if (fused) launch_embed_ln(dt, W.tok_emb_f32 ? (const void*)W.tok_emb_f32 : W.tok_emb, W.tok_emb_f32 != nullptr, W.pos_d, tok, pos, n_tok, d, dx, W.dec[0].ln1_w, W.dec[0].ln1_b, dh, st);
     else {
         launch_embed(dt, W.tok_emb_f32 ? (const void*)W.tok_emb_f32 : W.tok_emb, W.tok_emb_f32 != nullptr, W.pos_d, tok, pos, n_tok, d, dx, st);
@@ -950,14 +1059,6 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         if (splits <= 0) WM_FAIL("decode partials GEMM not applicable");
         return DecSlabs{v.splitk, splits, (long)n_tok * N, N, bias, scale};
     };
-    // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
-    // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
-    const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
-    if (fused && !w8 && ((c->quant && n_tok <= quant_small_max()) || n_tok <= small_m_max()) && gemm_small_ok(n_tok, d, true) &&
-        gemm_small_ok(n_tok, 4 * d, false)) {
-        decoder_rows_small(c, s, v, xdirect, self_share, kt_stride);
-        return;
-    }
     for (int l = 0; l < L; l++) {
         const int lw = l;
         LayerW Lw = W.dec[lw];
@@ -1452,10 +1553,12 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     const bool any = logits_prepare(S, act, false);
     whisper_state::DecGraph* G = nullptr;
     const int sig = dec_path_sig();
+    const bool pd = pdec_use(c, s, n, s->direct);
     for (auto& g : s->dec_graphs)
-        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig) G = &g;
+        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd)
+            G = &g;
     if (!G) {
-        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, nullptr, {}};
+        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, nullptr, {}};
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
@@ -1468,9 +1571,41 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         s->dec_graphs.push_back(std::move(g));
         G = &s->dec_graphs.back();
     }
-    WM_CHECK(hipGraphLaunch(G->exec, s->stream));
-    logits_finish(S, n, any, probs_rows);
+    if (!G->pdec) {
+        WM_CHECK(hipGraphLaunch(G->exec, s->stream));
+        logits_finish(S, n, any, probs_rows);
+        kt_flush_graph(s, *G);
+        return;
+    }
+    // A persistent launch needs its 256 workgroups resident together: persistent steps of different
+    // states (threads) of this process never overlap, so two of them cannot hold half the CUs each.
+    static std::mutex pdec_run_mu;
+    bool gave_up;
+    {
+        std::lock_guard<std::mutex> lk(pdec_run_mu);
+        WM_CHECK(hipGraphLaunch(G->exec, s->stream));
+        logits_finish(S, n, any, probs_rows);
+        gave_up = *s->ws.h_pd_err != 0;
+    }
     kt_flush_graph(s, *G);
+    if (!gave_up) return;
+    // the launch gave up (a wait timed out: not every workgroup became resident): the step again on
+    // the per-kernel path, which rewrites everything the launch may have written (the self K/V rows of
+    // this position)
+    static bool warned = false;
+    if (!warned) fprintf(stderr, "whisper_mi355x: persistent decode step timed out; step re-run on the per-kernel path\n");
+    warned = true;
+    *s->ws.h_pd_err = 0;
+    s->pdec_block = true;
+    try {
+        decoder_launch(c, s, n, n, true, s->direct);
+        logits_launch(c, s, n);
+        logits_finish(S, n, any, probs_rows);
+    } catch (...) {
+        s->pdec_block = false;
+        throw;
+    }
+    s->pdec_block = false;
 }
 
 // Batches above kPairMin clips run as two independent halves at

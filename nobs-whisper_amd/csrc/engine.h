@@ -104,6 +104,9 @@ struct Context {
     // (logits), the cross-attention K/V weights and prefill keep the compute type
     struct Fp8Dec { void *wqkv, *wo, *wxq, *wxo, *w1, *w2; float *sqkv, *so, *sxq, *sxo, *s1, *s2; };
     std::vector<Fp8Dec> dec8;
+    // persistent decode step (kernels/pdec.hip): the decoder layers' pointers as a device array
+    std::mutex pdec_mu;
+    void* pdec_layers = nullptr;
     // States released by whisper_free_state, kept with their workspace and captured decode graphs
     // for the next whisper_init_state: whisper.rs:83-85 creates (and drops) a state on every
     // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.
@@ -158,6 +161,10 @@ struct Workspace {
     TokOut* tout = nullptr;
     void* lrec = nullptr;  // split logits kernel: per-chunk records
     int *win_job = nullptr, *win_seek = nullptr, *win_slot = nullptr;
+    // persistent decode step: in-launch hand-off buffers, counters, and the error word's host copy
+    float* pd = nullptr;
+    unsigned* pd_sync = nullptr;
+    unsigned* h_pd_err = nullptr;
     // mel / pcm
     float* pcm = nullptr;
     float* mel = nullptr;
@@ -177,7 +184,7 @@ struct Job;
 
 // Live per-kernel-class timing with HIP events on the state's stream (bench.py's roofline leg).
 // `work` is the algorithmic FLOPs (MFMA-bound classes) or HBM bytes (HBM-bound classes).
-enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_OTHER, K_NCLASS };
+enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_PDEC, K_OTHER, K_NCLASS };
 struct KStat { double ms = 0, work = 0; long count = 0; };
 
 }  // namespace wm
@@ -217,11 +224,12 @@ struct whisper_state {
     // decode steps replayed as hipGraphs, one per (active-clip count, timing mask, cross form, path
     // signature): `sig` encodes the per-call switches that pick the step's kernels (dec_path_sig), so a
     // changed setting never replays a graph captured for another path
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; hipGraphExec_t exec; std::vector<KPending> ev; };
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; bool pdec; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step
     whisper_state* twin = nullptr;                // second half of a paired batch (full_batch)
+    bool pdec_block = false;                      // re-running a step whose persistent launch gave up
 };
 
 struct whisper_context {

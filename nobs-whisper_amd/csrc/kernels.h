@@ -173,6 +173,42 @@ void launch_xattn_step(DType dt, const void* enc, const int* slot, const void* q
 void launch_xattn_combine(DType dt, const float* opart, const float* ml, int splits, const void* wv, const float* bv, int n,
                           int d, int H, void* out, hipStream_t st);
 
+// ---- persistent decode step (kernels/pdec.hip) ---------------------------------------------------
+// One launch = every decoder layer of one decode step for M <= kPdecMaxRows clips in the cross K/V cache
+// form, phases handed off through sharded counters (see pdec.hip). Output: out_dh [M][d] (T) = the final
+// LayerNorm of each row, the logits GEMM's input.
+constexpr int kPdecMaxRows = 4;
+struct PdecLayer {
+    const void *wqkv, *wo, *wxq, *wxo, *w1, *w2;
+    const float *bqkv, *bo, *bxq, *bxo, *b1, *b2;
+    const float *ln1_w, *ln1_b, *lnx_w, *lnx_b, *ln2_w, *ln2_b;
+};
+struct PdecArgs {
+    const PdecLayer* layers;  // device array [L]
+    int L, M, d, n_text_ctx, n_audio_ctx;
+    const void* tok_emb; int te_f32; const float* pos_d;
+    const float *lnd_w, *lnd_b;
+    const int *tok, *pos, *slot;      // [M]
+    void* self_cache; const void* cross_cache;
+    float k_scale;
+    float *x0, *x1, *x2, *qkv, *qx, *ff;  // in-launch hand-off buffers: [M][d] x3, [M][3d], [M][d], [M][4d]
+    float *spart, *xpart;               // attention partials [256][68]
+    int s_self, s_cross;                // key splits per (clip, head)
+    unsigned* sync;                     // pdec_sync_bytes(L), zeroed by the launcher; last word: error
+    void* out_dh;
+    const uint16_t* gelu_tab;           // ggml's f16 GELU table on the device (gelu_table_device)
+    long spin_ticks;                    // a wait gives up after this many 100 MHz ticks (g_pdec_spin_ticks)
+};
+// 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
+extern long g_pdec_spin_ticks;
+bool pdec_supported(int d, int H);
+size_t pdec_sync_bytes(int L);
+int pdec_splits(int M, int H, int rows);
+// error word of the sync block (a non-zero value: the launch gave up, results invalid)
+inline size_t pdec_err_offset(int L) { return ((size_t)(L + 1) * 8 * 8) * sizeof(unsigned); }
+void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st);
+const uint16_t* gelu_table_device();
+
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {
     int n_vocab, eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, space, n_lang;

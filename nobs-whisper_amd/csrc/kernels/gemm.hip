@@ -54,6 +54,12 @@ void init_gelu_table() {
     WM_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_gelu_tab), tab.data(), tab.size() * sizeof(uint16_t)));
 }
 
+const uint16_t* gelu_table_device() {
+    void* p = nullptr;
+    WM_CHECK(hipGetSymbolAddress(&p, HIP_SYMBOL(g_gelu_tab)));
+    return (const uint16_t*)p;
+}
+
 // == gelu_ggml(x), bit for bit
 __device__ __forceinline__ float gelu_tab(float x) {
     if (x <= -10.0f) return 0.0f;

@@ -150,13 +150,7 @@ def _gpu_logits(wrs, dtype):
     return _GPU_LG[dtype]
 
 
-@pytest.mark.parametrize("dtype", ["F16", "BF16"])
-@pytest.mark.parametrize("k", range(len(SPOT)))
-def test_largev3_b128_teacher_forced(wrs, monkeypatch, dtype, k):
-    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
-    clip = SPOT[k]
-    ref = _oracle_logits(clip)
-    got = _gpu_logits(wrs, dtype)[:, k, :]
+def _check(dtype, clip, got, ref, label):
     assert np.isfinite(got).all()
     d = np.abs(got.astype(np.float64) - ref)
     per_step = d.max(axis=1)
@@ -165,7 +159,7 @@ def test_largev3_b128_teacher_forced(wrs, monkeypatch, dtype, k):
     top2 = np.sort(ref, axis=1)[:, -2:]
     gap = top2[:, 1] - top2[:, 0]
     flips = [(i, float(gap[i])) for i in range(N_TOK) if int(np.argmax(got[i])) != int(np.argmax(ref[i]))]
-    print(f"large-v3 {dtype} b128 clip {clip}: worst step |dlogit| {per_step.max():.4f} (step {int(per_step.argmax())}), "
+    print(f"large-v3 {dtype} {label} clip {clip}: worst step |dlogit| {per_step.max():.4f} (step {int(per_step.argmax())}), "
           f"relative {rel.max():.2e}, median relative {np.median(rel):.2e}, logit scale {scale.mean():.1f}, "
           f"argmax flips {flips}")
     if dtype == "F16":
@@ -173,3 +167,46 @@ def test_largev3_b128_teacher_forced(wrs, monkeypatch, dtype, k):
     else:
         assert per_step.max() <= BF16_DEEP_TOL, (per_step.max(), int(per_step.argmax()))
         assert all(g <= 2 * BF16_DEEP_TOL for _, g in flips), flips
+
+
+_FEW_LG = {}
+
+
+@pytest.mark.parametrize("dtype", ["F16", "BF16"])
+@pytest.mark.parametrize("n_clips", [1, 4])
+def test_largev3_few_clips_teacher_forced(wrs, monkeypatch, dtype, n_clips):
+    """The app's pattern at full depth: 1 (and 4) clips, the cross K/V cache form, every step one
+    persistent launch (kernels/pdec.hip; its kernel class counts the launches), teacher-forced along the
+    oracle's fixed-work sequences of the spot clips: the same bars as the 128-clip case."""
+    from conftest import model_path
+    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
+    spot = SPOT[:n_clips]
+    key = (dtype, n_clips)
+    if key not in _FEW_LG:
+        seqs = np.array([_oracle_seq(c) for c in spot], np.int32)
+        ctx = wrs.WhisperContext(model_path("large-v3+conf"), dtype=getattr(wrs, dtype))
+        st = ctx.create_state()
+        L = wrs.lib()
+        L.whisper_mi355x_kernel_timing(st.ptr, 1 << 7)
+        V = L.whisper_n_vocab(ctx.ptr)
+        rc, lg = st.full_batch_forced(wrs.reference_full_params("en"), [synthetic_pcm(c) for c in spot], N_TOK, seqs,
+                                      list(range(n_clips)), V)
+        assert rc == 0, rc
+        import ctypes as C
+        out = (C.c_double * 3)()
+        L.whisper_mi355x_kernel_stats(st.ptr, 7, out)
+        assert not st.info()["direct"] and out[1] >= N_TOK - 1, (st.info(), out[1])
+        st.close()
+        ctx.close()
+        _FEW_LG[key] = lg
+    for k, c in enumerate(spot):
+        _check(dtype, c, _FEW_LG[key][:, k, :], _oracle_logits(c), f"persistent b{n_clips}")
+
+
+@pytest.mark.parametrize("dtype", ["F16", "BF16"])
+@pytest.mark.parametrize("k", range(len(SPOT)))
+def test_largev3_b128_teacher_forced(wrs, monkeypatch, dtype, k):
+    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
+    clip = SPOT[k]
+    ref = _oracle_logits(clip)
+    _check(dtype, clip, _gpu_logits(wrs, dtype)[:, k, :], ref, "b128")

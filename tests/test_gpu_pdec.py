@@ -1,0 +1,165 @@
+"""The persistent decode step (nobs-whisper_amd/csrc/kernels/pdec.hip): every decoder layer of a decode
+step of <= 4 clips (the app's one clip per call, whisper.rs:83-85 / state.rs:147) in ONE launch, the
+cross K/V cache form.
+
+  * whisper_full f16 through it: token ids, timestamps, text and per-window decisions identical to the
+    oracle on every model width the kernel is built for (d 384 / 512 / 768 / 1280; 1024 is in
+    tests/test_gpu_fulldepth.py), with the reference's FullParams, prompted and auto-language cases;
+  * a batch of 4 clips (the largest it takes) against the oracle clip by clip;
+  * the give-up path: with a zero spin limit every launch gives up and the step is re-run on the
+    per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit;
+  * two states on two host threads (persistent steps serialised by the engine): each equals its
+    single-threaded run.
+Each case checks that the persistent kernel actually ran (its kernel-timing class counted launches).
+"""
+import threading
+
+import pytest
+
+from make_model import synthetic_pcm
+from oracle_py import Oracle, reference_params
+
+pytestmark = pytest.mark.gpu
+
+K_PDEC = 7
+_REF = {}
+
+
+def oracle_full(shape, clip, lang="en", prompt=None, t_inc=0.2):
+    from conftest import model_path
+    key = (shape, clip, lang, prompt, t_inc)
+    if key not in _REF:
+        o = Oracle(model_path(shape), mode=1, n_threads=16)
+        rp = reference_params(lang, prompt=prompt)
+        rp.temperature_inc = t_inc
+        _REF[key] = o.full(synthetic_pcm(clip), rp)
+        o.close()
+    return _REF[key]
+
+
+def ints(segs):
+    return [([t[0] for t in s.tokens], s.t0, s.t1) for s in segs]
+
+
+def ref_ints(ref):
+    return [(s["tokens"], s["t0"], s["t1"]) for s in ref["segments"]]
+
+
+DEC_KEYS = ("seek", "temp_idx", "failed0", "logprob_fail0", "result_len0", "no_speech")
+
+
+def pdec_launches(wrs, st):
+    import ctypes as C
+    out = (C.c_double * 3)()
+    assert wrs.lib().whisper_mi355x_kernel_stats(st.ptr, K_PDEC, out) == 0
+    return int(out[1])
+
+
+CASES = [("tiny.en+conf", 0, "en", None), ("tiny.en+conf", 1, None, None), ("base+conf", 0, "en", None),
+         ("base+conf", 1, "en", "DEFAULT"), ("small-4L+conf", 0, "en", None), ("large-v3-2L+conf", 0, "en", None),
+         ("large-v3-2L+conf", 0, None, "DEFAULT")]
+
+
+@pytest.mark.parametrize("shape,clip,lang,prompt", CASES)
+def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt):
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    prompt = wrs.DEFAULT_VOCABULARY if prompt == "DEFAULT" else prompt
+    ref = oracle_full(shape, clip, lang, prompt)
+    assert all(d["temp_idx"] == 0 for d in ref["decisions"]), ref["decisions"]
+    ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
+    st = ctx.create_state()
+    wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
+    assert st.full(wrs.reference_full_params(lang, initial_prompt=prompt), synthetic_pcm(clip)) == 0
+    n = pdec_launches(wrs, st)
+    segs, dec = st.segments(), st.decisions()
+    st.close()
+    ctx.close()
+    assert n > 0, "the persistent decode step did not run"
+    assert ints(segs) == ref_ints(ref)
+    assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
+    assert [tuple(d[k] for k in DEC_KEYS) for d in dec] == [tuple(d[k] for k in DEC_KEYS) for d in ref["decisions"]]
+    print(f"{shape} clip {clip}: {n} persistent steps, {sum(len(s['tokens']) for s in ref['segments'])} tokens identical")
+
+
+def test_pdec_batch4_vs_oracle(wrs, monkeypatch):
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    shape = "base+conf"
+    ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
+    st = ctx.create_state()
+    wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
+    p = wrs.reference_full_params("en")
+    p.temperature_inc = 0.0
+    assert st.full_batch(p, [synthetic_pcm(k) for k in range(4)]) == 0
+    assert pdec_launches(wrs, st) > 0
+    for j in range(4):
+        ref = oracle_full(shape, j, "en", None, t_inc=0.0)
+        assert ints(st.batch_segments(j)) == ref_ints(ref), j
+    st.close()
+    ctx.close()
+
+
+def _run(wrs, path, clips, dtype):
+    ctx = wrs.WhisperContext(path, dtype=dtype)
+    st = ctx.create_state()
+    wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
+    assert st.full_batch(wrs.reference_full_params("en"), clips) == 0
+    out = [ints(st.batch_segments(j)) for j in range(len(clips))], [st.decisions(j) for j in range(len(clips))]
+    n = pdec_launches(wrs, st)
+    st.close()
+    ctx.close()
+    return out, n
+
+
+@pytest.mark.parametrize("dtype", ["F16", "BF16"])
+def test_pdec_give_up_reruns_step(wrs, monkeypatch, capfd, dtype):
+    """Zero spin limit: every persistent launch gives up at its first wait; the engine re-runs each
+    step on the per-kernel path, so the results are those of WHISPER_MI355X_PDEC=0 exactly."""
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    monkeypatch.setenv("WHISPER_MI355X_STATE_POOL", "0")
+    path = model_path("tiny+conf")
+    clips = [synthetic_pcm(k) for k in range(2)]
+    L = wrs.lib()
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")
+    plain, n0 = _run(wrs, path, clips, getattr(wrs, dtype))
+    assert n0 == 0
+    monkeypatch.delenv("WHISPER_MI355X_PDEC")
+    L.whisper_mi355x_set_pdec_spin(0)
+    try:
+        forced, n1 = _run(wrs, path, clips, getattr(wrs, dtype))
+    finally:
+        L.whisper_mi355x_set_pdec_spin(5000000)
+    assert n1 > 0
+    assert forced == plain
+
+
+def test_pdec_two_threads(wrs, monkeypatch):
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    path = model_path("base+conf")
+    ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+    clips = [synthetic_pcm(k) for k in range(2)]
+    p = wrs.reference_full_params("en")
+    single = []
+    for c in clips:
+        st = ctx.create_state()
+        assert st.full(p, c) == 0
+        single.append(ints(st.segments()))
+        st.close()
+    res = [None, None]
+
+    def work(i):
+        st = ctx.create_state()
+        rc = st.full(p, clips[i])
+        res[i] = (rc, ints(st.segments()))
+        st.close()
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    ctx.close()
+    assert [r[0] for r in res] == [0, 0]
+    assert [r[1] for r in res] == single
