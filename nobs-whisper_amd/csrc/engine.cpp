@@ -836,6 +836,18 @@ static const PdecLayer* pdec_layers(Context* c) {
     return (const PdecLayer*)c->pdec_layers;
 }
 
+// Everything a persistent step allocates, before a decode step is captured (no hipMalloc in a capture)
+static void pdec_prepare(Context* c, whisper_state* s) {
+    Workspace& w = s->ws;
+    pdec_layers(c);
+    if (w.pd) return;
+    const size_t pd_floats = (size_t)kPdecMaxRows * 10 * c->hp.n_text_state + 2 * 256 * 68;
+    dalloc(w.pd, pd_floats * sizeof(float));
+    dalloc(w.pd_sync, pdec_sync_bytes(c->hp.n_text_layer));
+    WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
+    *w.h_pd_err = 0;
+}
+
 // One decode step of the view's rows as the persistent launch + the logits GEMM (graph-capturable).
 // The launch's error word is copied to the host (a node of the step's graph): decode_step checks it
 // after the step's synchronisation and re-runs the step on the per-kernel path if the launch gave up.
@@ -845,15 +857,9 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab;
     const int n = v.n;
     hipStream_t st = v.st;
-    const size_t pd_floats = (size_t)kPdecMaxRows * 10 * d + 2 * 256 * 68;
-    if (!w.pd) {
-        dalloc(w.pd, pd_floats * sizeof(float));
-        dalloc(w.pd_sync, pdec_sync_bytes(L));
-        WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
-        *w.h_pd_err = 0;
-    }
+    if (!w.pd || !c->pdec_layers) WM_FAIL("pdec: buffers not allocated (pdec_prepare)");
     PdecArgs a{};
-    a.layers = pdec_layers(c);
+    a.layers = (const PdecLayer*)c->pdec_layers;
     a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.n_audio_ctx = hp.n_audio_ctx;
     a.tok_emb = c->w.tok_emb_f32 ? (const void*)c->w.tok_emb_f32 : c->w.tok_emb;
     a.te_f32 = c->w.tok_emb_f32 != nullptr;
@@ -1554,6 +1560,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     whisper_state::DecGraph* G = nullptr;
     const int sig = dec_path_sig();
     const bool pd = pdec_use(c, s, n, s->direct);
+    if (pd) pdec_prepare(c, s);
     for (auto& g : s->dec_graphs)
         if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd)
             G = &g;

@@ -55,9 +55,12 @@ void init_gelu_table() {
 }
 
 const uint16_t* gelu_table_device() {
-    void* p = nullptr;
-    WM_CHECK(hipGetSymbolAddress(&p, HIP_SYMBOL(g_gelu_tab)));
-    return (const uint16_t*)p;
+    static const uint16_t* p = [] {
+        void* q = nullptr;
+        WM_CHECK(hipGetSymbolAddress(&q, HIP_SYMBOL(g_gelu_tab)));
+        return (const uint16_t*)q;
+    }();
+    return p;
 }
 
 // == gelu_ggml(x), bit for bit

@@ -55,22 +55,27 @@ def pdec_launches(wrs, st):
     return int(out[1])
 
 
-CASES = [("tiny.en+conf", 0, "en", None), ("tiny.en+conf", 1, None, None), ("base+conf", 0, "en", None),
-         ("base+conf", 1, "en", "DEFAULT"), ("small-4L+conf", 0, "en", None), ("large-v3-2L+conf", 0, "en", None),
-         ("large-v3-2L+conf", 0, None, "DEFAULT")]
+# the reference's FullParams (temperature_inc 0.2) where the oracle decides every window at t = 0 (the
+# cases of tests/test_gpu_configs.py F16_CASES), greedy-only (0.0) for small-4L
+CASES = [("tiny.en+conf", 0, "en", "DEFAULT", 0.2), ("tiny.en+conf", 1, None, None, 0.2), ("base+conf", 0, "en", None, 0.2),
+         ("base+conf", 1, "en", "DEFAULT", 0.2), ("small-4L+conf", 0, "en", None, 0.0),
+         ("large-v3-2L+conf", 0, "en", None, 0.2), ("large-v3-2L+conf", 1, None, None, 0.2),
+         ("large-v3-2L+conf", 0, None, "DEFAULT", 0.2)]
 
 
-@pytest.mark.parametrize("shape,clip,lang,prompt", CASES)
-def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt):
+@pytest.mark.parametrize("shape,clip,lang,prompt,t_inc", CASES)
+def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc):
     from conftest import model_path
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
     prompt = wrs.DEFAULT_VOCABULARY if prompt == "DEFAULT" else prompt
-    ref = oracle_full(shape, clip, lang, prompt)
+    ref = oracle_full(shape, clip, lang, prompt, t_inc)
     assert all(d["temp_idx"] == 0 for d in ref["decisions"]), ref["decisions"]
     ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
     st = ctx.create_state()
     wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
-    assert st.full(wrs.reference_full_params(lang, initial_prompt=prompt), synthetic_pcm(clip)) == 0
+    gp = wrs.reference_full_params(lang, initial_prompt=prompt)
+    gp.temperature_inc = t_inc
+    assert st.full(gp, synthetic_pcm(clip)) == 0
     n = pdec_launches(wrs, st)
     segs, dec = st.segments(), st.decisions()
     st.close()
