@@ -841,7 +841,8 @@ static void pdec_prepare(Context* c, whisper_state* s) {
     Workspace& w = s->ws;
     pdec_layers(c);
     if (w.pd) return;
-    const size_t pd_floats = (size_t)kPdecMaxRows * 10 * c->hp.n_text_state + 2 * 256 * 68;
+    // x0, x1, x2 (3d) + qkv (3d) + qx (d) + ff (4d) = 11d per row, + two partial buffers
+    const size_t pd_floats = (size_t)kPdecMaxRows * 11 * c->hp.n_text_state + 2 * 256 * 68;
     dalloc(w.pd, pd_floats * sizeof(float));
     dalloc(w.pd_sync, pdec_sync_bytes(c->hp.n_text_layer));
     WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
@@ -877,7 +878,8 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.qx = p; p += R * d;
     a.ff = p; p += R * 4 * d;
     a.spart = p; p += 256 * 68;
-    a.xpart = p;
+    a.xpart = p; p += 256 * 68;
+    if ((size_t)(p - w.pd) > (size_t)kPdecMaxRows * 11 * d + 2 * 256 * 68) WM_FAIL("pdec: scratch layout");
     a.s_self = pdec_splits(n, H, hp.n_text_ctx);
     a.s_cross = pdec_splits(n, H, hp.n_audio_ctx);
     a.sync = w.pd_sync;
