@@ -4,7 +4,8 @@ cross K/V cache form.
 
   * whisper_full f16 through it: token ids, timestamps, text and per-window decisions identical to the
     oracle on every model width the kernel is built for (d 384 / 512 / 768 / 1280; 1024 is in
-    tests/test_gpu_fulldepth.py), with the reference's FullParams, prompted and auto-language cases;
+    tests/test_gpu_fulldepth.py), with the reference's FullParams, prompted and auto-language cases
+    (a clip with an oracle near tie <= F16_GAP nats: identical up to that step);
   * a batch of 4 clips (the largest it takes) against the oracle clip by clip;
   * the give-up path: with a zero spin limit every launch gives up and the step is re-run on the
     per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit;
@@ -17,11 +18,16 @@ import threading
 import pytest
 
 from make_model import synthetic_pcm
+from margin_gate import assert_diverges_only_at_close_calls, kept_token_margins
 from oracle_py import Oracle, reference_params
 
 pytestmark = pytest.mark.gpu
 
 K_PDEC = 7
+# f16 is compared exactly on clips whose every greedy step the oracle decided by more than F16_GAP nats
+# (f16 teacher-forced logits sit within ~0.015 of the oracle's, tests/test_gpu_fulldepth.py); where the
+# oracle itself has a near tie, exactly up to that step (the round-2 rule)
+F16_GAP = 0.05
 _REF = {}
 
 
@@ -81,10 +87,17 @@ def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
     st.close()
     ctx.close()
     assert n > 0, "the persistent decode step did not run"
-    assert ints(segs) == ref_ints(ref)
-    assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
-    assert [tuple(d[k] for k in DEC_KEYS) for d in dec] == [tuple(d[k] for k in DEC_KEYS) for d in ref["decisions"]]
-    print(f"{shape} clip {clip}: {n} persistent steps, {sum(len(s['tokens']) for s in ref['segments'])} tokens identical")
+    exp, margins = kept_token_margins(ref)
+    if min(margins) > F16_GAP:
+        assert ints(segs) == ref_ints(ref)
+        assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
+        assert [tuple(d[k] for k in DEC_KEYS) for d in dec] == [tuple(d[k] for k in DEC_KEYS) for d in ref["decisions"]]
+        print(f"{shape} clip {clip}: {n} persistent steps, {len(exp)} tokens identical")
+    else:  # the oracle decided a step by <= F16_GAP nats: exact up to the first such near tie
+        got = [t for sg in ints(segs) for t in sg[0]]
+        k = assert_diverges_only_at_close_calls(got, exp, margins, F16_GAP, 4)
+        print(f"{shape} clip {clip}: {n} persistent steps, {k} of {len(exp)} tokens identical "
+              f"(oracle near tie {min(margins):.4f} nats)")
 
 
 def test_pdec_batch4_vs_oracle(wrs, monkeypatch):
