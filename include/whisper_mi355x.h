@@ -127,6 +127,10 @@ WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
  * 50 ms); 0 makes every persistent launch give up, so each step takes the re-run path. Captured graphs
  * keep the value they were captured with. */
 WHISPER_API void whisper_mi355x_set_pdec_spin(long ticks);
+/* Profiling hook: device buffer of 256 * n_text_layer * 8 * 2 u64 that persistent decode steps captured
+ * from now on fill with the 100 MHz clock (per workgroup, layer and phase: input arrived, phase
+ * signalled); NULL turns it off. */
+WHISPER_API void whisper_mi355x_set_pdec_stamps(void * dev);
 /* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
  * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */
 // fp8 (OCP e4m3) GEMM with per-row f32 scales (A per row m, B per row n), then epilogue `epi`;

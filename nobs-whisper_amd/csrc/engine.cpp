@@ -803,10 +803,10 @@ static int dec_path_sig() {
 }
 
 // A decode step of n clips runs as one persistent launch when the model shape has a kernel, the
-// weights are plain f16 / bf16 (not blocks, not the fp8 decoder copies), the device has the 256 CUs
-// the grid is built for, and the step is in the cross K/V cache form.
+// weights are f16 / bf16 or GGML blocks (not the fp8 decoder copies), the device has the 256 CUs the
+// grid is built for, and the step is in the cross K/V cache form.
 static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
-    if (xdirect || s->pdec_block || n < 1 || n > pdec_max() || c->quant) return false;
+    if (xdirect || s->pdec_block || n < 1 || n > pdec_max()) return false;
     if (c->fp8_enc && !c->dec8.empty()) return false;
     if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head)) return false;
     static const int cus = [] {
@@ -825,7 +825,11 @@ static const PdecLayer* pdec_layers(Context* c) {
         std::vector<PdecLayer> h(c->hp.n_text_layer);
         for (int l = 0; l < c->hp.n_text_layer; l++) {
             const LayerW& L = c->w.dec[l];
-            h[l] = PdecLayer{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2, L.bqkv, L.bo, L.bxq, L.bxo, L.b1, L.b2,
+            auto mat = [](const void* w, const QMat& q) {
+                return q.type ? PdecMat{q.qs, q.qh, q.dm, q.type} : PdecMat{w, nullptr, nullptr, 0};
+            };
+            h[l] = PdecLayer{mat(L.wqkv, L.qqkv), mat(L.wo, L.qo), mat(L.wxq, L.qxq), mat(L.wxo, L.qxo), mat(L.w1, L.q1),
+                             mat(L.w2, L.q2), L.bqkv, L.bo, L.bxq, L.bxo, L.b1, L.b2,
                              L.ln1_w, L.ln1_b, L.lnx_w, L.lnx_b, L.ln2_w, L.ln2_b};
         }
         void* p = nullptr;
@@ -886,6 +890,7 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
     a.gelu_tab = gelu_table_device();
     a.spin_ticks = g_pdec_spin_ticks;
+    a.stamps = g_pdec_stamps;
     {
         // weights once + cross K/V + self K/V of every row, per launch
         const double bytes = 14.0 * d * d * 2 * L + (double)n * L * 2 * hp.n_audio_ctx * d * 2 + s->cur_self_work;

@@ -178,8 +178,16 @@ void launch_xattn_combine(DType dt, const float* opart, const float* ml, int spl
 // form, phases handed off through sharded counters (see pdec.hip). Output: out_dh [M][d] (T) = the final
 // LayerNorm of each row, the logits GEMM's input.
 constexpr int kPdecMaxRows = 4;
+// one projection matrix [N][K]: the compute type (qt = 0, w = T weights) or GGML blocks (qt = ggml type,
+// w = QMat::qs, qh, dm as in QMat)
+struct PdecMat {
+    const void* w;
+    const uint32_t* qh;
+    const uint16_t* dm;
+    int qt;
+};
 struct PdecLayer {
-    const void *wqkv, *wo, *wxq, *wxo, *w1, *w2;
+    PdecMat qkv, o, xq, xo, f1, f2;
     const float *bqkv, *bo, *bxq, *bxo, *b1, *b2;
     const float *ln1_w, *ln1_b, *lnx_w, *lnx_b, *ln2_w, *ln2_b;
 };
@@ -198,7 +206,9 @@ struct PdecArgs {
     void* out_dh;
     const uint16_t* gelu_tab;           // ggml's f16 GELU table on the device (gelu_table_device)
     long spin_ticks;                    // a wait gives up after this many 100 MHz ticks (g_pdec_spin_ticks)
+    unsigned long long* stamps;         // debug (g_pdec_stamps): [256][L][8][2] clock at input / signal, or null
 };
+extern unsigned long long* g_pdec_stamps;
 // 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
 extern long g_pdec_spin_ticks;
 bool pdec_supported(int d, int H);

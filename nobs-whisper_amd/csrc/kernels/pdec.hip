@@ -144,25 +144,86 @@ __device__ __forceinline__ bool pd_wait(unsigned* sync, unsigned* err, int idx, 
 // Projection over the WG's column slice [c0, c1) of an [N][K] matrix: wave w takes columns c0 + w + 4 j
 // (j < NCW), lane l the 16-byte vectors l + 64 v (v < NV) of each column. Weights are loaded into
 // registers by `load` (before the phase's wait) and multiplied by `run` with the M rows staged in LDS.
+// 8 weights of a GGML block (weights 8g .. 8g+7; r = {qs bytes 8(g&1) .. +7 (q4/q5) or 8g .. +7 (q8),
+// q5 high bits, d | m << 16}) -> T, ggml's dequantize_row_* arithmetic (exact in f32, one rounding):
+// gemm.hip qraw_deq with the type at run time
+template <typename T>
+__device__ __forceinline__ void deq8(int qt, uint32_t b0, uint32_t b1, uint32_t qh, uint32_t dm, int g, float (&wf)[8]) {
+    const float dd = (float)__builtin_bit_cast(half_t, (uint16_t)(dm & 0xFFFF));
+    const float mm = (float)__builtin_bit_cast(half_t, (uint16_t)(dm >> 16));
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t byte = ((i < 4 ? b0 : b1) >> (8 * (i & 3))) & 0xFF;
+        float v;
+        if (qt == 8) {
+            v = (float)(int8_t)byte * dd;
+        } else {
+            int x = (g >> 1) ? (int)(byte >> 4) : (int)(byte & 15);
+            if (qt == 6 || qt == 7) x |= (int)((qh >> (8 * g + i)) & 1) << 4;
+            if (qt == 3 || qt == 7) v = (float)x * dd + mm;
+            else v = (float)(x - (qt == 6 ? 16 : 8)) * dd;
+        }
+        wf[i] = (float)(T)v;
+    }
+}
+
+// Projection over the WG's column slice [c0, c1) of an [N][K] matrix: wave w takes columns c0 + w + 4 j
+// (j < NCW). Plain weights: lane l the 16-byte vectors l + 64 v (v < NV) of each column. GGML blocks
+// (PdecMat.qt != 0): lane l the 32-weight blocks l + 64 v (v < NB = NV / 3) of each column, their quant
+// bytes in slots 2v (and 2v + 1 for q8_0) and {q5 high bits, d | m << 16} in slot 2 NB + v. Weights are
+// loaded into registers by `load` (before the phase's wait) and multiplied by `run` with the M rows
+// staged in LDS.
 template <typename T, int NCW, int NV>
 struct ColSlice {
+    static constexpr int NB = NV / 3;
     u32x4 w[NCW][NV];
-    int c0, nc, K;
-    __device__ __forceinline__ void load(const T* __restrict__ W, int N, int K_) {
+    int c0, nc, K, qt;
+    __device__ __forceinline__ void load(const PdecMat& W, int N, int K_) {
         K = K_;
+        qt = W.qt;
         const int w0 = blockIdx.x;
         c0 = (int)((long)w0 * N / kG);
         nc = (int)((long)(w0 + 1) * N / kG) - c0;
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const int nvec = K >> 3;
+        if (qt == 0) {
+            const int nvec = K >> 3;
+#pragma unroll
+            for (int j = 0; j < NCW; j++) {
+                const int cl = wave + 4 * j;
+                const T* row = (const T*)W.w + (long)(c0 + (cl < nc ? cl : 0)) * K;
+#pragma unroll
+                for (int v = 0; v < NV; v++) {
+                    const int vi = lane + 64 * v;
+                    w[j][v] = (cl < nc && vi < nvec) ? __builtin_nontemporal_load(gp((const u32x4*)(row + vi * 8)))
+                                                     : (u32x4){0, 0, 0, 0};
+                }
+            }
+            return;
+        }
+        const int nblk = K >> 5;
+        const uint8_t* qs = (const uint8_t*)W.w;
 #pragma unroll
         for (int j = 0; j < NCW; j++) {
             const int cl = wave + 4 * j;
-            const T* row = W + (long)(c0 + (cl < nc ? cl : 0)) * K;
+            const long n = c0 + (cl < nc ? cl : 0);
 #pragma unroll
-            for (int v = 0; v < NV; v++) {
-                const int vi = lane + 64 * v;
-                w[j][v] = (cl < nc && vi < nvec) ? __builtin_nontemporal_load(gp((const u32x4*)(row + vi * 8))) : (u32x4){0, 0, 0, 0};
+            for (int v = 0; v < NB; v++) {
+                const int bi = lane + 64 * v;
+                u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0}, meta = {0, 0, 0, 0};
+                if (cl < nc && bi < nblk) {
+                    const long blk = n * nblk + bi;
+                    if (qt == 8) {
+                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi)));
+                        b = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi + 16)));
+                    } else {
+                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * (K / 2) + 16L * bi)));
+                    }
+                    meta.x = (qt == 6 || qt == 7) ? *gp(W.qh + blk) : 0u;
+                    meta.y = (qt == 3 || qt == 7) ? *gp((const uint32_t*)W.dm + blk) : (uint32_t)*gp(W.dm + blk);
+                }
+                w[j][2 * v] = a;
+                w[j][2 * v + 1] = b;
+                w[j][2 * NB + v] = meta;
             }
         }
     }
@@ -170,31 +231,55 @@ struct ColSlice {
     template <int MAXM>
     __device__ __forceinline__ void run(const T* xs, int ldx, int M, float (&acc)[NCW][MAXM]) const {
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const int nvec = K >> 3;
 #pragma unroll
         for (int j = 0; j < NCW; j++)
 #pragma unroll
             for (int m = 0; m < MAXM; m++) acc[j][m] = 0.0f;
+        auto fma8 = [&](const float (&wf)[8], int j, int koff) {
 #pragma unroll
-        for (int v = 0; v < NV; v++) {
-            const int vi = lane + 64 * v;
-            if (vi >= nvec) break;
+            for (int m = 0; m < MAXM; m++) {
+                if (m >= M) break;
+                const u32x4 xv = *(const u32x4*)(xs + (long)m * ldx + koff);
+                const T* xe = (const T*)&xv;
+                float acc_ = acc[j][m];
 #pragma unroll
-            for (int j = 0; j < NCW; j++) {
-                // one weight vector widened at a time (the prefetched weights stay packed in registers)
-                float wf[8];
-                const T* we = (const T*)&w[j][v];
+                for (int e = 0; e < 8; e++) acc_ = __builtin_fmaf((float)xe[e], wf[e], acc_);
+                acc[j][m] = acc_;
+            }
+        };
+        if (qt == 0) {
+            const int nvec = K >> 3;
 #pragma unroll
-                for (int e = 0; e < 8; e++) wf[e] = (float)we[e];
+            for (int v = 0; v < NV; v++) {
+                const int vi = lane + 64 * v;
+                if (vi >= nvec) break;
 #pragma unroll
-                for (int m = 0; m < MAXM; m++) {
-                    if (m >= M) break;
-                    const u32x4 xv = *(const u32x4*)(xs + (long)m * ldx + vi * 8);
-                    const T* xe = (const T*)&xv;
-                    float acc_ = acc[j][m];
+                for (int j = 0; j < NCW; j++) {
+                    // one weight vector widened at a time (the prefetched weights stay packed in registers)
+                    float wf[8];
+                    const T* we = (const T*)&w[j][v];
 #pragma unroll
-                    for (int e = 0; e < 8; e++) acc_ = __builtin_fmaf((float)xe[e], wf[e], acc_);
-                    acc[j][m] = acc_;
+                    for (int e = 0; e < 8; e++) wf[e] = (float)we[e];
+                    fma8(wf, j, vi * 8);
+                }
+            }
+        } else {
+            const int nblk = K >> 5;
+#pragma unroll
+            for (int v = 0; v < NB; v++) {
+                const int bi = lane + 64 * v;
+                if (bi >= nblk) break;
+#pragma unroll
+                for (int j = 0; j < NCW; j++) {
+                    const u32x4 a = w[j][2 * v], b = w[j][2 * v + 1], meta = w[j][2 * NB + v];
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        float wf[8];
+                        const uint32_t b0 = qt == 8 ? (g < 2 ? a[2 * g] : b[2 * g - 4]) : a[2 * (g & 1)];
+                        const uint32_t b1 = qt == 8 ? (g < 2 ? a[2 * g + 1] : b[2 * g - 3]) : a[2 * (g & 1) + 1];
+                        deq8<T>(qt, b0, b1, meta.x, meta.y, g, wf);
+                        fma8(wf, j, bi * 32 + g * 8);
+                    }
                 }
             }
         }
@@ -259,25 +344,41 @@ __device__ __forceinline__ void ln_rows(const float* x, int M, const float* __re
 }
 
 // Merge the attention partials of every (row, head) (S splits each) into xs (T [M][D], LDS): thread
-// per (row, head, 4 dims); o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
+// per (row, head, 4 dims); o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s. Branch-free, the loads of
+// 8 splits issued together (an empty split holds m = -inf, l = 0, o = 0 and gets weight 0).
 template <typename T, int D>
 __device__ __forceinline__ void merge_parts(const float* part, int M, int S, T* xs) {
     constexpr int H = D / 64;
     const __amdgpu_buffer_rsrc_t r = rsrc(part);
     for (int q = threadIdx.x; q < M * H * 16; q += kNT) {
         const int mh = q >> 4, j4 = (q & 15) * 4;
-        const float* p0 = part + (long)mh * S * kPartStride;
+        const int base = mh * S * kPartStride;
         float mx = -INFINITY;
-        for (int s = 0; s < S; s++) mx = fmaxf(mx, ld_sc1(p0 + s * kPartStride));
+        for (int s0 = 0; s0 < S; s0 += 8) {
+            float ms[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) ms[u] = s0 + u < S ? ld_sc1(part + base + (s0 + u) * kPartStride) : -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 8; u++) mx = fmaxf(mx, ms[u]);
+        }
         float L = 0.0f;
         float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int s = 0; s < S; s++) {
-            const float ms = ld_sc1(p0 + s * kPartStride);
-            if (ms == -INFINITY) continue;
-            const float wgt = __expf(ms - mx);
-            L += wgt * ld_sc1(p0 + s * kPartStride + 1);
-            const float4 os = ld4_sc1(r, (int)(((long)mh * S + s) * kPartStride + 4 + j4) * 4);
-            o.x += wgt * os.x; o.y += wgt * os.y; o.z += wgt * os.z; o.w += wgt * os.w;
+        for (int s0 = 0; s0 < S; s0 += 8) {
+            float2 ml[8];
+            float4 os[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int sb = base + min(s0 + u, S - 1) * kPartStride;
+                const float4 h = ld4_sc1(r, sb * 4);  // m, l, pad, pad
+                ml[u] = make_float2(h.x, h.y);
+                os[u] = ld4_sc1(r, (sb + 4 + j4) * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const float wgt = (s0 + u < S && ml[u].x != -INFINITY) ? __expf(ml[u].x - mx) : 0.0f;
+                L += wgt * ml[u].y;
+                o.x += wgt * os[u].x; o.y += wgt * os[u].y; o.z += wgt * os[u].z; o.w += wgt * os[u].w;
+            }
         }
         const float inv = 1.0f / L;
         const int m = mh / H, h = mh % H;
@@ -288,31 +389,49 @@ __device__ __forceinline__ void merge_parts(const float* part, int M, int S, T* 
 
 // One attention task: query q (64 f32 in LDS), keys/values rows [r0, r1) of (K, V) [rows][64] T, plus,
 // if fresh >= 0 and in range, row `fresh` taken from fk / fv (LDS f32) instead of the cache. Writes the
-// partial {max, sum, 0, 0, o[64]} (f32) to out with sc1 stores.
+// partial {max, sum, 0, 0, o[64]} (f32) to out with sc1 stores. 32 lane groups of 8 lanes, a key row
+// per group and U rows in flight per group (every load of a chunk issued before its first use; the
+// first V chunk is issued under the softmax).
 template <typename T>
 __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, int r0, int r1,
                                           int fresh, const float* fk, const float* fv, float* sc, float* red, float* out) {
     const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
-    constexpr int NG = kNT / 8;
+    constexpr int NG = kNT / 8, U = 8, CH = NG * U;
+    const u32x4 zero = {0, 0, 0, 0};
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
-    float lmax = -INFINITY;
-    for (int t = r0 + grp; t < r1; t += NG) {
-        float a = 0.0f;
-        if (t == fresh) {
+    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
-        } else {
-            const u32x4 raw = *gp((const u32x4*)(K + (long)t * 64 + lane8 * 8));
-            const T* ke = (const T*)&raw;
-#pragma unroll
-            for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            raw[u] = (t < r1 && t != fresh) ? *gp((const u32x4*)(base + (long)t * 64 + lane8 * 8)) : zero;
         }
-        a = sum8(a);
-        if (lane8 == 0) sc[t - r0] = a;
-        lmax = fmaxf(lmax, a);
+    };
+    float lmax = -INFINITY;
+    u32x4 raw[U];
+    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
+        load_rows(K, t0, raw);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            const T* ke = (const T*)&raw[u];
+            float a = 0.0f;
+            if (t == fresh) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+            }
+            a = sum8(a);
+            if (t < r1) {
+                if (lane8 == 0) sc[t - r0] = a;
+                lmax = fmaxf(lmax, a);
+            }
+        }
     }
+    load_rows(V, r0 + grp, raw);  // the first V chunk lands under the softmax
     lmax = wave_max(lmax);
     if (lane == 0) red[wave] = lmax;
     __syncthreads();
@@ -329,16 +448,21 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    for (int t = r0 + grp; t < r1; t += NG) {
-        const float p = sc[t - r0];
-        if (t == fresh) {
+    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
+        if (t0 != r0 + grp) load_rows(V, t0, raw);
 #pragma unroll
-            for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
-        } else {
-            const u32x4 raw = *gp((const u32x4*)(V + (long)t * 64 + lane8 * 8));
-            const T* ve = (const T*)&raw;
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            if (t >= r1) break;
+            const float p = sc[t - r0];
+            if (t == fresh) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+                for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
+            } else {
+                const T* ve = (const T*)&raw[u];
+#pragma unroll
+                for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+            }
         }
     }
     // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by shuffles, then over the 4 waves in LDS
@@ -368,8 +492,9 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
 template <typename T, int D, int MAXM>
 __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     constexpr int H = D / 64;
-    constexpr int NV1 = (D / 8 + 63) / 64;          // vectors per lane per column at K = d
-    constexpr int NV4 = (4 * D / 8 + 63) / 64;      // at K = 4d
+    // register slots per lane per column: 16-byte vectors of plain weights, or 3 per 32-weight block
+    constexpr int NV1 = std::max((D / 8 + 63) / 64, 3 * ((D / 32 + 63) / 64));          // K = d
+    constexpr int NV4 = std::max((4 * D / 8 + 63) / 64, 3 * ((4 * D / 32 + 63) / 64));  // K = 4d
     constexpr int CQ = (3 * D + kG - 1) / kG, C1 = (D + kG - 1) / kG, C4 = (4 * D + kG - 1) / kG;
     constexpr int NCQ = (CQ + 3) / 4, NC1 = (C1 + 3) / 4, NC4 = (C4 + 3) / 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -389,6 +514,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     const __amdgpu_buffer_rsrc_t rff = rsrc(a.ff);
 
     auto idx = [&](int l, int p) { return l * kPhases + p; };
+    // debug: per (WG, layer, phase) the 100 MHz clock when the phase's input arrived and when it signalled
+    auto stamp = [&](int l, int p, int k) {
+        if (a.stamps && tid == 0) a.stamps[(((long)w0 * a.L + l) * kPhases + p) * 2 + k] = __builtin_amdgcn_s_memrealtime();
+    };
     // residual of the WG's own columns: x_old (sc1, or the embedding at layer 0) + v
     auto x_old = [&](const float* x, int l, int m, int n) -> float {
         if (l == 0 && x == a.x0) {
@@ -403,8 +532,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         // ---- A: LN1 + QKV ------------------------------------------------------------------------------
         {
             ColSlice<T, NCQ, NV1> cs;
-            cs.load((const T*)W.wqkv, 3 * D, D);
+            cs.load(W.qkv, 3 * D, D);
             if (l > 0 && !pd_wait(sync, err, idx(l, P_X0), lflag, a.spin_ticks)) return;
+            stamp(l, 0, 0);
             ln_rows<T, D>(a.x0, M, W.ln1_w, W.ln1_b, xs, l == 0, te, te32, a.pos_d, a.tok, a.pos);
             __syncthreads();
             float acc[NCQ][MAXM];
@@ -422,10 +552,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l, P_QKV));
+            stamp(l, 0, 1);
         }
         // ---- B: self attention -----------------------------------------------------------------------------
         {
             if (!pd_wait(sync, err, idx(l, P_QKV), lflag, a.spin_ticks)) return;
+            stamp(l, 1, 0);
             const int S = a.s_self;
             if (w0 < M * H * S) {
                 const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
@@ -444,12 +576,14 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                              a.spart + (long)w0 * kPartStride);
             }
             pd_signal(sync, idx(l, P_SELF));
+            stamp(l, 1, 1);
         }
         // ---- C: merge + out projection + residual ------------------------------------------------------------
         {
             ColSlice<T, NC1, NV1> cs;
-            cs.load((const T*)W.wo, D, D);
+            cs.load(W.o, D, D);
             if (!pd_wait(sync, err, idx(l, P_SELF), lflag, a.spin_ticks)) return;
+            stamp(l, 2, 0);
             merge_parts<T, D>(a.spart, M, a.s_self, xs);
             __syncthreads();
             float acc[NC1][MAXM];
@@ -466,12 +600,14 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l, P_X1));
+            stamp(l, 2, 1);
         }
         // ---- D: LN + cross-Q projection --------------------------------------------------------------------
         {
             ColSlice<T, NC1, NV1> cs;
-            cs.load((const T*)W.wxq, D, D);
+            cs.load(W.xq, D, D);
             if (!pd_wait(sync, err, idx(l, P_X1), lflag, a.spin_ticks)) return;
+            stamp(l, 3, 0);
             ln_rows<T, D>(a.x1, M, W.lnx_w, W.lnx_b, xs, false, te, te32, a.pos_d, a.tok, a.pos);
             __syncthreads();
             float acc[NC1][MAXM];
@@ -487,10 +623,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l, P_XQ));
+            stamp(l, 3, 1);
         }
         // ---- E: cross attention over the cached K/V --------------------------------------------------------
         {
             if (!pd_wait(sync, err, idx(l, P_XQ), lflag, a.spin_ticks)) return;
+            stamp(l, 4, 0);
             const int S = a.s_cross;
             if (w0 < M * H * S) {
                 const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
@@ -504,12 +642,14 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 attn_task<T>(qf, Kc, Vc, r0, r1, -1, nullptr, nullptr, sc, red, a.xpart + (long)w0 * kPartStride);
             }
             pd_signal(sync, idx(l, P_XATT));
+            stamp(l, 4, 1);
         }
         // ---- F: merge + cross-out projection + residual ---------------------------------------------------------
         {
             ColSlice<T, NC1, NV1> cs;
-            cs.load((const T*)W.wxo, D, D);
+            cs.load(W.xo, D, D);
             if (!pd_wait(sync, err, idx(l, P_XATT), lflag, a.spin_ticks)) return;
+            stamp(l, 5, 0);
             merge_parts<T, D>(a.xpart, M, a.s_cross, xs);
             __syncthreads();
             float acc[NC1][MAXM];
@@ -526,12 +666,14 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l, P_X2));
+            stamp(l, 5, 1);
         }
         // ---- G: LN + FC1 + GELU ------------------------------------------------------------------------------
         {
             ColSlice<T, NC4, NV1> cs;
-            cs.load((const T*)W.w1, 4 * D, D);
+            cs.load(W.f1, 4 * D, D);
             if (!pd_wait(sync, err, idx(l, P_X2), lflag, a.spin_ticks)) return;
+            stamp(l, 6, 0);
             ln_rows<T, D>(a.x2, M, W.ln2_w, W.ln2_b, xs, false, te, te32, a.pos_d, a.tok, a.pos);
             __syncthreads();
             float acc[NC4][MAXM];
@@ -547,12 +689,14 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l, P_FF));
+            stamp(l, 6, 1);
         }
         // ---- H: FC2 + residual ----------------------------------------------------------------------------------
         {
             ColSlice<T, NC1, NV4> cs;
-            cs.load((const T*)W.w2, D, 4 * D);
+            cs.load(W.f2, D, 4 * D);
             if (!pd_wait(sync, err, idx(l, P_FF), lflag, a.spin_ticks)) return;
+            stamp(l, 7, 0);
             for (int q = tid; q < M * D; q += kNT) {  // the GELU rows (f32 values of T) -> LDS as T
                 const float4 v = ld4_sc1(rff, q * 16);
                 T* dst = xs + (long)q * 4;
@@ -573,6 +717,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             pd_signal(sync, idx(l + 1, P_X0));
+            stamp(l, 7, 1);
         }
     }
     // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
@@ -583,6 +728,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
 }
 
 long g_pdec_spin_ticks = 5000000;
+unsigned long long* g_pdec_stamps = nullptr;
 
 bool pdec_supported(int d, int H) { return H * 64 == d && (d == 384 || d == 512 || d == 768 || d == 1024 || d == 1280); }
 
