@@ -808,7 +808,13 @@ static int dec_path_sig() {
 static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
     if (xdirect || s->pdec_block || n < 1 || n > pdec_max()) return false;
     if (c->fp8_enc && !c->dec8.empty()) return false;
-    if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head)) return false;
+    // one weight form for every decoder matrix (the kernel is built per form)
+    const bool quant = c->w.dec[0].qqkv.type != 0;
+    for (const LayerW& L : c->w.dec)
+        for (const QMat* q : {&L.qqkv, &L.qo, &L.qxq, &L.qxo, &L.q1, &L.q2})
+            if ((q->type != 0) != quant) return false;
+    if (quant && c->dt != DType::F16) return false;
+    if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head, quant)) return false;
     static const int cus = [] {
         int dev = 0, v = 0;
         hipGetDevice(&dev);
@@ -845,10 +851,9 @@ static void pdec_prepare(Context* c, whisper_state* s) {
     Workspace& w = s->ws;
     pdec_layers(c);
     if (w.pd) return;
-    // x0, x1, x2 (3d) + qkv (3d) + qx (d) + ff (4d) = 11d per row, + two partial buffers
-    const size_t pd_floats = (size_t)kPdecMaxRows * 11 * c->hp.n_text_state + 2 * 256 * 68;
-    dalloc(w.pd, pd_floats * sizeof(float));
-    dalloc(w.pd_sync, pdec_sync_bytes(c->hp.n_text_layer));
+    // the cross-attention partials; the hand-off block
+    dalloc(w.pd, (size_t)256 * 68 * sizeof(float));
+    dalloc(w.pd_sync, pdec_granules(c->hp.n_text_state, c->hp.n_text_layer, c->hp.n_text_head).bytes);
     WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
     *w.h_pd_err = 0;
 }
@@ -873,20 +878,11 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
     a.self_cache = w.self; a.cross_cache = w.cross;
     a.k_scale = c->k_scale;
-    float* p = w.pd;
-    const size_t R = kPdecMaxRows;
-    a.x0 = p; p += R * d;
-    a.x1 = p; p += R * d;
-    a.x2 = p; p += R * d;
-    a.qkv = p; p += R * 3 * d;
-    a.qx = p; p += R * d;
-    a.ff = p; p += R * 4 * d;
-    a.spart = p; p += 256 * 68;
-    a.xpart = p; p += 256 * 68;
-    if ((size_t)(p - w.pd) > (size_t)kPdecMaxRows * 11 * d + 2 * 256 * 68) WM_FAIL("pdec: scratch layout");
-    a.s_self = pdec_splits(n, H, hp.n_text_ctx);
-    a.s_cross = pdec_splits(n, H, hp.n_audio_ctx);
+    a.xpart = w.pd;
+    a.quant = c->w.dec[0].qqkv.type != 0;
+    a.s_cross = pdec_cross_splits(n, H, hp.n_audio_ctx);
     a.sync = w.pd_sync;
+    a.gr = pdec_granules(d, L, H);
     a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
     a.gelu_tab = gelu_table_device();
     a.spin_ticks = g_pdec_spin_ticks;
@@ -897,7 +893,7 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
         KT kt(s, K_PDEC, bytes, st);
         launch_pdec(c->dt, a, st);
     }
-    WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + pdec_err_offset(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + a.gr.err_bytes, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
     tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }

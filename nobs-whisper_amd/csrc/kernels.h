@@ -175,7 +175,7 @@ void launch_xattn_combine(DType dt, const float* opart, const float* ml, int spl
 
 // ---- persistent decode step (kernels/pdec.hip) ---------------------------------------------------
 // One launch = every decoder layer of one decode step for M <= kPdecMaxRows clips in the cross K/V cache
-// form, phases handed off through sharded counters (see pdec.hip). Output: out_dh [M][d] (T) = the final
+// form, phases handed off through data-tagged granules (see pdec.hip). Output: out_dh [M][d] (T) = the final
 // LayerNorm of each row, the logits GEMM's input.
 constexpr int kPdecMaxRows = 4;
 // one projection matrix [N][K]: the compute type (qt = 0, w = T weights) or GGML blocks (qt = ggml type,
@@ -191,6 +191,15 @@ struct PdecLayer {
     const float *bqkv, *bo, *bxq, *bxo, *b1, *b2;
     const float *ln1_w, *ln1_b, *lnx_w, *lnx_b, *ln2_w, *ln2_b;
 };
+// The hand-off block (one allocation, zeroed before every launch): data-tagged 8-byte granules (offsets
+// in granules): x rows x0, x1, x2 [R][d] (f32), and packed T pairs: qkv [R][3d/2], self-attention output
+// so [R][d/2], cross q qx [R][d/2], cross-attention output xo [R][d/2], GELU rows ff [R][2d]; then the
+// cross-attention merge tickets [L][R][H] (u32) and the error word (byte offsets); R = kPdecMaxRows.
+struct PdecGranules {
+    long x0, x1, x2, qkv, so, qx, xo, ff;
+    long tick_bytes, err_bytes, bytes;
+};
+PdecGranules pdec_granules(int d, int L, int H);
 struct PdecArgs {
     const PdecLayer* layers;  // device array [L]
     int L, M, d, n_text_ctx, n_audio_ctx;
@@ -199,23 +208,23 @@ struct PdecArgs {
     const int *tok, *pos, *slot;      // [M]
     void* self_cache; const void* cross_cache;
     float k_scale;
-    float *x0, *x1, *x2, *qkv, *qx, *ff;  // in-launch hand-off buffers: [M][d] x3, [M][3d], [M][d], [M][4d]
-    float *spart, *xpart;               // attention partials [256][68]
-    int s_self, s_cross;                // key splits per (clip, head)
-    unsigned* sync;                     // pdec_sync_bytes(L), zeroed by the launcher; last word: error
+    float* xpart;                       // cross-attention partials [M * H * s_cross][68] (f32)
+    int s_cross;                        // key splits per (clip, head) of the cross attention
+    int quant;                          // the layers' matrices are GGML blocks (PdecMat.qt != 0)
+    void* sync;                         // the hand-off block (gr.bytes), zeroed by the launcher
+    PdecGranules gr;
     void* out_dh;
     const uint16_t* gelu_tab;           // ggml's f16 GELU table on the device (gelu_table_device)
     long spin_ticks;                    // a wait gives up after this many 100 MHz ticks (g_pdec_spin_ticks)
-    unsigned long long* stamps;         // debug (g_pdec_stamps): [256][L][8][2] clock at input / signal, or null
+    unsigned long long* stamps;         // debug (g_pdec_stamps): [256][L][8][2] clock at input / publish, or null
 };
 extern unsigned long long* g_pdec_stamps;
 // 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
 extern long g_pdec_spin_ticks;
-bool pdec_supported(int d, int H);
-size_t pdec_sync_bytes(int L);
-int pdec_splits(int M, int H, int rows);
-// error word of the sync block (a non-zero value: the launch gave up, results invalid)
-inline size_t pdec_err_offset(int L) { return ((size_t)(L + 1) * 8 * 8) * sizeof(unsigned); }
+// a kernel exists for the shape: plain weights at d 384 / 512 / 768 / 1024 / 1280, GGML blocks (f16
+// compute) at 768 / 1024 / 1280
+bool pdec_supported(int d, int H, bool quant);
+int pdec_cross_splits(int M, int H, int rows);
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st);
 const uint16_t* gelu_table_device();
 

@@ -1,0 +1,819 @@
+// Persistent decode step for few clips (the kernel; instantiated by pdec_f16.hip, pdec_bf16.hip, pdec_q.hip): the whole decoder (every layer) of one decode step in ONE
+// launch, its phases handing off through the L2 with counters instead of kernel boundaries
+// (the hot loop of whisper_full: whisper.rs:127-129 -> state.rs:147; the app
+// transcribes one clip per call, so this is the latency its user feels).
+//
+// Why: at one clip a large-v3 decoder layer streams 46 MB of weights +
+// 7.7 MB of cross K/V (~8 us at HBM speed) but took ~78 us as 8 dependent launches of 5-15 us each:
+// launch boundaries, ramp-up and dependent-load latency, not bytes. Here the grid is one 256-thread
+// workgroup per CU (G = 256), resident for the whole step:
+//   per layer, 8 phases:  A  LN1 + QKV projection (+ q/k scale, rounding to T)        all WGs, column slices
+//                         B  self attention over the cache, split over keys            (clip, head, split) tasks
+//                         C  split merge + out projection + residual                   all WGs
+//                         D  LN + cross-Q projection (+ scale)                         all WGs
+//                         E  cross attention over the cached K/V, split over keys      (clip, head, split) tasks
+//                         F  split merge + cross-out projection + residual             all WGs
+//                         G  LN + FC1 + GELU (ggml's f16 table)                       all WGs
+//                         H  FC2 + residual                                            all WGs
+//   then the final LayerNorm of every row (the logits GEMM is the next launch).
+// A projection phase: each WG owns a contiguous slice of output columns (N / G of them), so its weights
+// are ONE contiguous range of the [N][K] matrix; it issues their loads into registers BEFORE waiting for
+// the phase's input, so the weight stream of phase p overlaps the hand-off of phase p-1 (the loader-runs-
+// ahead idea of MI355X_MICROARCH.md "prefetch-credit", in registers instead of an LDS ring). Every WG
+// gathers the whole (small) input vector: M rows of d, computes the LayerNorm itself (ggml_norm: double
+// sums) and stages the rows in LDS as T; one wave per output column, lanes split K, f32 accumulation.
+//
+// Hand-offs (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility", Valid forms, table
+// row 1): every payload word is stored write-through (sc1) and drained (s_waitcnt vmcnt(0) in every
+// storing wave), the workgroup barrier, then ONE lane adds 1 to the phase's counter (agent-scope atomic),
+// sharded per XCD (8 words, blockIdx % 8) so 256 arrivals spread over 8 lines; the consumer's wave 0
+// polls the 8 shards with sc1 loads (+ s_sleep) until all G workgroups arrived, the workgroup barrier,
+// then EVERY load of a handed-off byte is an sc1 load (no acquire fence needed: the row's conditions
+// hold). Counters are per (layer, phase), zeroed by a memset node before every launch.
+// Bounded spins: a wait gives up after ~50 ms (s_memrealtime, 100 MHz), sets the error word and the
+// workgroup exits; every other wait sees the error word and exits too, so the grid always drains (e.g.
+// when another kernel holds CUs and not all 256 workgroups can be resident). The host then re-runs the
+// step on the launch-per-kernel path (engine.cpp), so a failed launch costs time, never results.
+//
+// Numerics (vs oracle/oracle_whisper.cpp, ggml's): LayerNorm as layernorm_kernel (double sums, separately
+// rounded ops, output rounded to T = ggml's f16 src1); projections f32-accumulated products of T
+// operands; q, k scaled by d_head^-0.25 then rounded to T, v rounded to T (the self cache holds T);
+// attention scores f32, softmax in f32 over each split with the split's own max, the unnormalised
+// weights rounded to T before P.V (ggml rounds the normalised P to f16: another rounding point, the
+// same precision), splits merged with exp(m_s - m) in f32 and the result rounded to T (the out
+// projection's src1). Results per row do not depend on the other rows' presence for a fixed (M, H):
+// the split count is a function of M (batch == single holds within the path at equal M only).
+#pragma once
+#include <algorithm>
+
+#include "../common.h"
+#include "../kernels.h"
+
+namespace wm {
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kG = 256;         // workgroups = CUs (one per CU)
+constexpr int kNT = 256;        // threads per workgroup
+constexpr int kPhases = 8;
+constexpr int kPartStride = 68; // floats per attention partial: m, l, pad x2, o[64]
+enum { P_X0 = 0, P_QKV, P_SELF, P_X1, P_XQ, P_XATT, P_X2, P_FF };
+
+// global (not flat) address space for the plain loads: flat loads also count in lgkmcnt
+template <typename P>
+__device__ __forceinline__ const __attribute__((address_space(1))) P* gp(const P* p) {
+    return (const __attribute__((address_space(1))) P*)p;
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0x7fffffff, 0x00020000);
+}
+// 16-byte sc1 load / store of a buffer written inside this launch (aux 16 = sc1)
+__device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+    return __builtin_bit_cast(float4, v);
+}
+__device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// sum over the 8 lanes of a key row (quad xor 1, quad xor 2, half-row mirror)
+__device__ __forceinline__ float sum8(float a) {
+    a += dppf<0xB1>(a);
+    a += dppf<0x4E>(a);
+    return a + dppf<0x141>(a);
+}
+__device__ __forceinline__ float wave_sum(float x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
+
+__device__ __forceinline__ float gelu_t(float x, const uint16_t* tab) {  // == gelu_ggml (gemm.hip gelu_tab)
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    return (float)__builtin_bit_cast(half_t, tab[__builtin_bit_cast(uint16_t, (half_t)x)]);
+}
+
+}  // namespace
+
+// ---- the kernel -----------------------------------------------------------------------------------------
+// Projection over the WG's column slice [c0, c1) of an [N][K] matrix: wave w takes columns c0 + w + 4 j
+// (j < NCW), lane l the 16-byte vectors l + 64 v (v < NV) of each column. Weights are loaded into
+// registers by `load` (before the phase's wait) and multiplied by `run` with the M rows staged in LDS.
+// 8 weights of a GGML block (weights 8g .. 8g+7; r = {qs bytes 8(g&1) .. +7 (q4/q5) or 8g .. +7 (q8),
+// q5 high bits, d | m << 16}) -> T, ggml's dequantize_row_* arithmetic (exact in f32, one rounding):
+// gemm.hip qraw_deq with the type at run time
+template <typename T>
+__device__ __forceinline__ void deq8(int qt, uint32_t b0, uint32_t b1, uint32_t qh, uint32_t dm, int g, float (&wf)[8]) {
+    const float dd = (float)__builtin_bit_cast(half_t, (uint16_t)(dm & 0xFFFF));
+    const float mm = (float)__builtin_bit_cast(half_t, (uint16_t)(dm >> 16));
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t byte = ((i < 4 ? b0 : b1) >> (8 * (i & 3))) & 0xFF;
+        float v;
+        if (qt == 8) {
+            v = (float)(int8_t)byte * dd;
+        } else {
+            int x = (g >> 1) ? (int)(byte >> 4) : (int)(byte & 15);
+            if (qt == 6 || qt == 7) x |= (int)((qh >> (8 * g + i)) & 1) << 4;
+            if (qt == 3 || qt == 7) v = (float)x * dd + mm;
+            else v = (float)(x - (qt == 6 ? 16 : 8)) * dd;
+        }
+        wf[i] = (float)(T)v;
+    }
+}
+
+// Projection over the WG's column slice [c0, c1) of an [N][K] matrix: wave w takes columns c0 + w + 4 j
+// (j < NCW). Plain weights: lane l the 16-byte vectors l + 64 v (v < NV) of each column. GGML blocks
+// (PdecMat.qt != 0): lane l the 32-weight blocks l + 64 v (v < NB = NV / 3) of each column, their quant
+// bytes in slots 2v (and 2v + 1 for q8_0) and {q5 high bits, d | m << 16} in slot 2 NB + v. Weights are
+// loaded into registers by `load` (before the phase's wait) and multiplied by `run` with the M rows
+// staged in LDS.
+template <typename T, int NCW, int NV, bool Q>
+struct ColSlice {
+    static constexpr int NB = NV / 3;
+    u32x4 w[NCW][NV];
+    int c0, nc, K, qt;
+    // pairs: slices of whole column pairs (2i, 2i + 1), for outputs handed off as packed T pairs
+    __device__ __forceinline__ void load(const PdecMat& W, int N, int K_, bool pairs) {
+        K = K_;
+        qt = Q ? W.qt : 0;
+        const int w0 = blockIdx.x, u = pairs ? 2 : 1, nu = N / u;
+        c0 = u * (int)((long)w0 * nu / kG);
+        nc = u * (int)((long)(w0 + 1) * nu / kG) - c0;
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (!Q) {
+            const int nvec = K >> 3;
+#pragma unroll
+            for (int j = 0; j < NCW; j++) {
+                const int cl = wave + 4 * j;
+                const T* row = (const T*)W.w + (long)(c0 + (cl < nc ? cl : 0)) * K;
+#pragma unroll
+                for (int v = 0; v < NV; v++) {
+                    const int vi = lane + 64 * v;
+                    w[j][v] = (cl < nc && vi < nvec) ? __builtin_nontemporal_load(gp((const u32x4*)(row + vi * 8)))
+                                                     : (u32x4){0, 0, 0, 0};
+                }
+            }
+            return;
+        }
+        const int nblk = K >> 5;
+        const uint8_t* qs = (const uint8_t*)W.w;
+#pragma unroll
+        for (int j = 0; j < NCW; j++) {
+            const int cl = wave + 4 * j;
+            const long n = c0 + (cl < nc ? cl : 0);
+#pragma unroll
+            for (int v = 0; v < NB; v++) {
+                const int bi = lane + 64 * v;
+                u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0}, meta = {0, 0, 0, 0};
+                if (cl < nc && bi < nblk) {
+                    const long blk = n * nblk + bi;
+                    if (qt == 8) {
+                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi)));
+                        b = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi + 16)));
+                    } else {
+                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * (K / 2) + 16L * bi)));
+                    }
+                    meta.x = (qt == 6 || qt == 7) ? *gp(W.qh + blk) : 0u;
+                    meta.y = (qt == 3 || qt == 7) ? *gp((const uint32_t*)W.dm + blk) : (uint32_t)*gp(W.dm + blk);
+                }
+                w[j][2 * v] = a;
+                w[j][2 * v + 1] = b;
+                w[j][2 * NB + v] = meta;
+            }
+        }
+    }
+    // acc[j][m] (all lanes) = sum_k xs[m][k] * W[c0 + wave + 4j][k]
+    template <int MAXM>
+    __device__ __forceinline__ void run(const T* xs, int ldx, int M, float (&acc)[NCW][MAXM]) const {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < NCW; j++)
+#pragma unroll
+            for (int m = 0; m < MAXM; m++) acc[j][m] = 0.0f;
+        auto fma8 = [&](const float (&wf)[8], int j, int koff) {
+#pragma unroll
+            for (int m = 0; m < MAXM; m++) {
+                if (m >= M) break;
+                const u32x4 xv = *(const u32x4*)(xs + (long)m * ldx + koff);
+                const T* xe = (const T*)&xv;
+                float acc_ = acc[j][m];
+#pragma unroll
+                for (int e = 0; e < 8; e++) acc_ = __builtin_fmaf((float)xe[e], wf[e], acc_);
+                acc[j][m] = acc_;
+            }
+        };
+        if (!Q) {
+            const int nvec = K >> 3;
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                const int vi = lane + 64 * v;
+                if (vi >= nvec) break;
+#pragma unroll
+                for (int j = 0; j < NCW; j++) {
+                    // one weight vector widened at a time (the prefetched weights stay packed in registers)
+                    float wf[8];
+                    const T* we = (const T*)&w[j][v];
+#pragma unroll
+                    for (int e = 0; e < 8; e++) wf[e] = (float)we[e];
+                    fma8(wf, j, vi * 8);
+                }
+            }
+        } else {
+            const int nblk = K >> 5;
+#pragma unroll
+            for (int v = 0; v < NB; v++) {
+                const int bi = lane + 64 * v;
+                if (bi >= nblk) break;
+#pragma unroll
+                for (int j = 0; j < NCW; j++) {
+                    const u32x4 a = w[j][2 * v], b = w[j][2 * v + 1], meta = w[j][2 * NB + v];
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        float wf[8];
+                        const uint32_t b0 = qt == 8 ? (g < 2 ? a[2 * g] : b[2 * g - 4]) : a[2 * (g & 1)];
+                        const uint32_t b1 = qt == 8 ? (g < 2 ? a[2 * g + 1] : b[2 * g - 3]) : a[2 * (g & 1) + 1];
+                        deq8<T>(qt, b0, b1, meta.x, meta.y, g, wf);
+                        fma8(wf, j, bi * 32 + g * 8);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NCW; j++)
+#pragma unroll
+            for (int m = 0; m < MAXM; m++)
+                if (m < M && wave + 4 * j < nc) acc[j][m] = wave_sum(acc[j][m]);
+    }
+};
+
+// LayerNorm of rows [0, M) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global): one wave per
+// row, layernorm_kernel's arithmetic (double sums, separately rounded ops)
+template <typename T, int D>
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __restrict__ w, const float* __restrict__ b, T* out) {
+#pragma clang fp contract(off)
+    constexpr int NPL = (D + 63) / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int m = wave; m < M; m += 4) {
+        float v[NPL];
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * e;
+            v[e] = k < D ? xf[m * D + k] : 0.0f;
+        }
+        double s = 0.0;
+#pragma unroll
+        for (int e = 0; e < NPL; e++) s += (double)v[e];
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const float mean = (float)(s / D);
+        double s2 = 0.0;
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * e;
+            v[e] = v[e] - mean;
+            if (k < D) s2 += (double)(v[e] * v[e]);
+        }
+        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+        const float variance = (float)(s2 / D);
+        const float scale = 1.0f / sqrtf(variance + 1e-5f);
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * e;
+            if (k < D) {
+                float t = v[e] * scale;
+                t = t * w[k];
+                out[(long)m * D + k] = (T)(t + b[k]);
+            }
+        }
+    }
+}
+
+// ---- hand-offs: data-tagged granules ----------------------------------------------------------------------
+// (MI355X_MICROARCH.md price table rows handoff-1to1 / allgather; cdna_hip_programming.md Guideline 16 R2)
+// Every handed-off value travels as ONE naturally aligned 8-byte granule {tag, 32 bits of data} written by
+// ONE sc1 store: the data is the flag, so a producer neither drains nor signals, and a consumer re-reads
+// the granules it needs (sc1 loads) until every tag equals the phase's tag = layer * 8 + phase + 1 (never 0).
+// The block is zeroed by a memset node before every launch. A buffer is reused by the next layer: safe
+// because every layer's phase A reads all of x0, i.e. waits for every workgroup's last phase of the layer
+// before, and every buffer of layer l + 1 is written after some workgroup's phase A of layer l + 1.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void put_g(unsigned long long* g, long i, unsigned tag, uint32_t bits) {
+    __hip_atomic_store((gu64*)(g + i), ((unsigned long long)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long get_g(const unsigned long long* g, long i) {
+    return __hip_atomic_load((gu64*)(g + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (T)lo) | ((uint32_t)__builtin_bit_cast(uint16_t, (T)hi) << 16);
+}
+template <typename T>
+__device__ __forceinline__ T lo_t(uint32_t v) { return __builtin_bit_cast(T, (uint16_t)(v & 0xFFFF)); }
+template <typename T>
+__device__ __forceinline__ T hi_t(uint32_t v) { return __builtin_bit_cast(T, (uint16_t)(v >> 16)); }
+
+// The workgroup waits for granules addr(0 .. n-1) of g to carry `tag` (every thread its own i = tid + kNT u,
+// 8 loads in flight per pass) and hands each granule's data to put(i, bits). A thread gives up after
+// spin_ticks (100 MHz) or when another workgroup set the error word; false = give up (the caller returns,
+// so every workgroup drains).
+template <typename A, typename P>
+__device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsigned tag, A addr, P put, unsigned* err,
+                                      int* lflag, long spin_ticks) {
+    constexpr int U = 8;
+    bool ok = true;
+    for (int b = 0; b < n && ok; b += kNT * U) {
+        unsigned long long v[U];
+        long t0 = 0;
+        for (int it = 0;; it++) {
+            bool done = true;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = b + threadIdx.x + kNT * u;
+                v[u] = i < n ? get_g(g, addr(i)) : (unsigned long long)tag << 32;
+                done &= (unsigned)(v[u] >> 32) == tag;
+            }
+            if (done) break;
+            const long now = (long)__builtin_amdgcn_s_memrealtime();
+            if (it == 0) t0 = now;
+            if (now - t0 > spin_ticks) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+            if ((it & 15) == 15 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (ok) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = b + threadIdx.x + kNT * u;
+                if (i < n) put(i, (uint32_t)v[u]);
+            }
+        }
+    }
+    if (!ok) *lflag = 0;  // set to 1 at the start; a workgroup that gave up exits, so it never goes back
+    __syncthreads();
+    const bool r = *lflag != 0;
+    __syncthreads();
+    return r;
+}
+
+// One attention task: query q (64 f32 in LDS), keys/values rows [r0, r1) of (K, V) [rows][64] T, plus,
+// if fresh >= 0 and in range, row `fresh` taken from fk / fv (LDS f32) instead of the cache. Leaves in res
+// (LDS): o[64] = sum_t p_t v_t, res[64] = max score, res[65] = sum_t p_t, with p_t = e^(s_t - max)
+// (rounded to T as the P.V operand). 32 lane groups of 8 lanes, a key row per group and U rows in flight
+// per group; a range of at most one chunk (32 U rows) issues its V rows together with its K rows.
+template <typename T, int U>
+__device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, int r0, int r1,
+                                          int fresh, const float* fk, const float* fv, float* sc, float* red, float* res) {
+    const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
+    constexpr int NG = kNT / 8, CH = NG * U;
+    const u32x4 zero = {0, 0, 0, 0};
+    float qv[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
+    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            raw[u] = (t < r1 && t != fresh) ? *gp((const u32x4*)(base + (long)t * 64 + lane8 * 8)) : zero;
+        }
+    };
+    const bool one = r1 - r0 <= CH;
+    float lmax = -INFINITY;
+    u32x4 rk[U], rv[U];
+    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
+        load_rows(K, t0, rk);
+        if (one) load_rows(V, t0, rv);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            const T* ke = (const T*)&rk[u];
+            float a = 0.0f;
+            if (t == fresh) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+            }
+            a = sum8(a);
+            if (t < r1) {
+                if (lane8 == 0) sc[t - r0] = a;
+                lmax = fmaxf(lmax, a);
+            }
+        }
+    }
+    if (!one) load_rows(V, r0 + grp, rv);  // the first V chunk lands under the softmax
+    lmax = wave_max(lmax);
+    if (lane == 0) red[wave] = lmax;
+    __syncthreads();
+    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float lsum = 0.0f;
+    for (int t = tid; t < r1 - r0; t += kNT) {
+        const float e = __expf(sc[t] - mx);
+        lsum += e;
+        sc[t] = (float)(T)e;  // unnormalised weight rounded to T (the P.V operand)
+    }
+    lsum = wave_sum(lsum);
+    __syncthreads();  // red[] read above by every wave, sc[] complete
+    if (lane == 0) red[wave] = lsum;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] = 0.0f;
+    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
+        if (t0 != r0 + grp) load_rows(V, t0, rv);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + NG * u;
+            if (t >= r1) break;
+            const float p = sc[t - r0];
+            if (t == fresh) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
+            } else {
+                const T* ve = (const T*)&rv[u];
+#pragma unroll
+                for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+            }
+        }
+    }
+    // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by shuffles, then over the 4 waves in LDS
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        acc[e] += __shfl_xor(acc[e], 8);
+        acc[e] += __shfl_xor(acc[e], 16);
+        acc[e] += __shfl_xor(acc[e], 32);
+    }
+    __syncthreads();
+    float* ow = red + 8;  // [4 waves][64]
+    if (lane < 8) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) ow[wave * 64 + lane * 8 + e] = acc[e];
+    }
+    __syncthreads();
+    if (tid < 64) {
+        res[tid] = (ow[tid] + ow[64 + tid]) + (ow[128 + tid] + ow[192 + tid]);
+        if (tid == 0) {
+            res[64] = mx;
+            res[65] = (red[0] + red[1]) + (red[2] + red[3]);
+        }
+    }
+    __syncthreads();
+}
+
+template <typename T, int D, int MAXM, bool Q>
+__global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
+    constexpr int H = D / 64;
+    // register slots per lane per column: 16-byte vectors of plain weights, or 3 per 32-weight block
+    constexpr int NV1 = Q ? 3 * ((D / 32 + 63) / 64) : (D / 8 + 63) / 64;          // K = d
+    constexpr int NV4 = Q ? 3 * ((4 * D / 32 + 63) / 64) : (4 * D / 8 + 63) / 64;  // K = 4d
+    // columns per workgroup: single columns (x rows, f32 granules) or pairs (packed T granules)
+    constexpr int C1 = (D + kG - 1) / kG;
+    constexpr int CQ = 2 * ((3 * D / 2 + kG - 1) / kG), CX = 2 * ((D / 2 + kG - 1) / kG), C4 = 2 * ((2 * D + kG - 1) / kG);
+    constexpr int NC1 = (C1 + 3) / 4, NCQ = (CQ + 3) / 4, NCX = (CX + 3) / 4, NC4 = (C4 + 3) / 4;
+    constexpr int CMAX = std::max(CQ, C4);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* xs = (T*)smem;                                                 // [M][4d] T: the projections' rows
+    float* xf = (float*)(smem + (size_t)MAXM * 4 * D * sizeof(T));    // [M][d] f32: a handed-off x row
+    float* sc = xf + MAXM * D;                                        // scores [1536]
+    float* red = sc + 1536;                                           // [8 + 256]
+    float* qf = red + 8 + 256;                                        // q, fresh k, fresh v [3][64]
+    float* res = qf + 192;                                            // attention result [64 + 2] (+ pad)
+    float* ost = res + 68;                                            // packed outputs [M][CMAX]
+    int* lflag = (int*)(ost + MAXM * CMAX);
+
+    const int M = a.M, L = a.L, w0 = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const PdecGranules& G = a.gr;
+    unsigned long long* gb = (unsigned long long*)a.sync;
+    unsigned long long *g_x0 = gb + G.x0, *g_x1 = gb + G.x1, *g_x2 = gb + G.x2, *g_qkv = gb + G.qkv;
+    unsigned long long *g_so = gb + G.so, *g_qx = gb + G.qx, *g_xo = gb + G.xo, *g_ff = gb + G.ff;
+    unsigned* tick = (unsigned*)((char*)a.sync + G.tick_bytes);
+    unsigned* err = (unsigned*)((char*)a.sync + G.err_bytes);
+    const T* te = (const T*)a.tok_emb;
+    const float* te32 = a.te_f32 ? (const float*)a.tok_emb : nullptr;
+    const T* self = (const T*)a.self_cache;
+    const T* cross = (const T*)a.cross_cache;
+    const long spin = a.spin_ticks;
+    if (tid == 0) *lflag = 1;
+
+    auto tag = [&](int l, int p) { return (unsigned)(l * 8 + p + 1); };
+    // debug: per (WG, layer, phase) the 100 MHz clock when the phase's input arrived and when it published
+    auto stamp = [&](int l, int p, int k) {
+        if (a.stamps && tid == 0) a.stamps[(((long)w0 * a.L + l) * 8 + p) * 2 + k] = __builtin_amdgcn_s_memrealtime();
+    };
+    auto f32_of = [](uint32_t b) { return __builtin_bit_cast(float, b); };
+    // sweeps of a whole buffer into LDS: x rows (f32) -> xf, packed T rows of width 2 * nw -> xs (row stride 2 * nw)
+    auto sweep_xf = [&](unsigned long long* g, unsigned tg) {
+        return sweep(g, M * D, tg, [](int i) { return (long)i; }, [&](int i, uint32_t b) { xf[i] = f32_of(b); }, err, lflag, spin);
+    };
+    auto sweep_xs = [&](unsigned long long* g, int nw, unsigned tg) {
+        return sweep(g, M * nw, tg, [](int i) { return (long)i; },
+                     [&](int i, uint32_t b) { xs[2 * i] = lo_t<T>(b); xs[2 * i + 1] = hi_t<T>(b); }, err, lflag, spin);
+    };
+    // packed outputs: lane m of wave w holds column c0 + w + 4 j of row m; staged in LDS, then one granule per pair
+    auto publish_pairs = [&](unsigned long long* g, int nw, int c0, int nc, unsigned tg) {
+        __syncthreads();
+        const int np = nc >> 1;
+        for (int q = tid; q < M * np; q += kNT) {
+            const int m = q / np, pi = q % np;
+            put_g(g, (long)m * nw + (c0 >> 1) + pi, tg, pack2<T>(ost[m * CMAX + 2 * pi], ost[m * CMAX + 2 * pi + 1]));
+        }
+    };
+
+    // the residual stream of the workgroup's own columns (c1_0 + wave + 4 j), lane m holding row m
+    const int c1_0 = (int)((long)w0 * D / kG), c1_n = (int)((long)(w0 + 1) * D / kG) - c1_0;
+    float xcur[NC1][MAXM];
+
+    ColSlice<T, NCQ, NV1, Q> wq;
+    ColSlice<T, NC1, NV1, Q> wo, wxo;
+    ColSlice<T, NCX, NV1, Q> wxq;
+    ColSlice<T, NC4, NV1, Q> wf1;
+    ColSlice<T, NC1, NV4, Q> wf2;
+    wq.load(a.layers[0].qkv, 3 * D, D, true);
+
+    for (int l = 0; l < L; l++) {
+        const PdecLayer& W = a.layers[l];
+        // ---- A: LN1 + QKV (q, k scaled; rounded to T) ----------------------------------------------------------
+        {
+            if (l == 0) {  // token + position embedding (embed_kernel's arithmetic)
+                for (int i = tid; i < M * D; i += kNT) {
+                    const int m = i / D, k = i % D;
+                    const long t = a.tok[m], p = a.pos[m];
+                    xf[i] = (te32 ? te32[t * D + k] : (float)te[t * D + k]) + a.pos_d[p * D + k];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NC1; j++)
+#pragma unroll
+                    for (int m = 0; m < MAXM; m++) {
+                        const int cl = wave + 4 * j;
+                        xcur[j][m] = (m < M && cl < c1_n) ? xf[m * D + c1_0 + cl] : 0.0f;
+                    }
+            } else if (!sweep_xf(g_x0, tag(l, 0))) {
+                return;
+            }
+            stamp(l, 0, 0);
+            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs);
+            __syncthreads();
+            float acc[NCQ][MAXM];
+            wq.template run<MAXM>(xs, D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NCQ; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wq.nc && lane == m) {
+                        const int n = wq.c0 + cl;
+                        float v = acc[j][m] + W.bqkv[n];
+                        if (n < 2 * D) v = v * a.k_scale;
+                        ost[m * CMAX + cl] = (float)(T)v;
+                    }
+                }
+            publish_pairs(g_qkv, 3 * D / 2, wq.c0, wq.nc, tag(l, 1));
+            stamp(l, 0, 1);
+        }
+        // ---- B: self attention of (row, head) over the cache + this position (one task each) ----------------
+        {
+            wo.load(W.o, D, D, false);
+            if (w0 < M * H) {
+                const int m = w0 / H, h = w0 % H;
+                // q, k, v of head h: granules h * 32 + i of each third of the row
+                if (!sweep(g_qkv, 96, tag(l, 1), [&](int i) { return (long)m * (3 * D / 2) + (i >> 5) * (D / 2) + h * 32 + (i & 31); },
+                           [&](int i, uint32_t b) {
+                               qf[2 * i] = (float)lo_t<T>(b);
+                               qf[2 * i + 1] = (float)hi_t<T>(b);
+                           }, err, lflag, spin))
+                    return;
+                stamp(l, 1, 0);
+                const int pos = a.pos[m], nkv = pos + 1;
+                const long sl = a.slot[m];
+                T* Kc = (T*)self + (((sl * L + l) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
+                T* Vc = (T*)self + (((sl * L + l) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
+                if (tid < 64) {  // append this position's k, v to the cache (read by the next steps' launches)
+                    Kc[(long)pos * 64 + tid] = (T)qf[64 + tid];
+                    Vc[(long)pos * 64 + tid] = (T)qf[128 + tid];
+                }
+                attn_task<T, 16>(qf, Kc, Vc, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
+                if (tid < 32) {
+                    const float inv = 1.0f / res[65];
+                    put_g(g_so, (long)m * (D / 2) + h * 32 + tid, tag(l, 2), pack2<T>(res[2 * tid] * inv, res[2 * tid + 1] * inv));
+                }
+                stamp(l, 1, 1);
+            }
+        }
+        // ---- C: out projection + residual -----------------------------------------------------------------------
+        {
+            wxq.load(W.xq, D, D, true);
+            if (!sweep_xs(g_so, D / 2, tag(l, 2))) return;
+            stamp(l, 2, 0);
+            float acc[NC1][MAXM];
+            wo.template run<MAXM>(xs, D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NC1; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wo.nc && lane == m) {
+                        const int n = wo.c0 + cl;
+                        xcur[j][m] = (acc[j][m] + W.bo[n]) + xcur[j][m];
+                        put_g(g_x1, (long)m * D + n, tag(l, 3), __builtin_bit_cast(uint32_t, xcur[j][m]));
+                    }
+                }
+            stamp(l, 2, 1);
+        }
+        // ---- D: LN + cross-Q projection (scaled; rounded to T) --------------------------------------------------
+        {
+            wxo.load(W.xo, D, D, false);
+            if (!sweep_xf(g_x1, tag(l, 3))) return;
+            stamp(l, 3, 0);
+            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs);
+            __syncthreads();
+            float acc[NCX][MAXM];
+            wxq.template run<MAXM>(xs, D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NCX; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wxq.nc && lane == m) {
+                        const int n = wxq.c0 + cl;
+                        ost[m * CMAX + cl] = (float)(T)((acc[j][m] + W.bxq[n]) * a.k_scale);
+                    }
+                }
+            publish_pairs(g_qx, D / 2, wxq.c0, wxq.nc, tag(l, 4));
+            stamp(l, 3, 1);
+        }
+        // ---- E: cross attention over the cached K/V, split over keys; the last split of a (row, head) merges ----
+        {
+            wf1.load(W.f1, 4 * D, D, true);
+            const int S = a.s_cross;
+            if (w0 < M * H * S) {
+                const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
+                if (!sweep(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
+                           [&](int i, uint32_t b) {
+                               qf[2 * i] = (float)lo_t<T>(b);
+                               qf[2 * i + 1] = (float)hi_t<T>(b);
+                           }, err, lflag, spin))
+                    return;
+                stamp(l, 4, 0);
+                const int T_ = a.n_audio_ctx;
+                const int r0 = (int)((long)s * T_ / S), r1 = (int)((long)(s + 1) * T_ / S);
+                const long sl = a.slot[m];
+                const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
+                const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
+                attn_task<T, 8>(qf, Kc, Vc, r0, r1, -1, nullptr, nullptr, sc, red, res);
+                // the partial {max, sum, 0, 0, o[64]}: sc1 stores, drained, then the (row, head) ticket
+                float* part = a.xpart + (long)w0 * kPartStride;
+                int* last = lflag + 1;
+                if (tid < 64) {
+                    st_sc1(part + 4 + tid, res[tid]);
+                    if (tid == 0) {
+                        st_sc1(part, res[64]);
+                        st_sc1(part + 1, res[65]);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+                if (tid == 0)
+                    *last = __hip_atomic_fetch_add(tick + ((long)l * MAXM + m) * H + h, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
+                __syncthreads();
+                if (*last) {
+                    // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s over the S partials (sc1 loads)
+                    const float* p0 = a.xpart + (long)(w0 - s) * kPartStride;
+                    if (tid < 64) {
+                        float mx = -INFINITY;
+                        for (int s0 = 0; s0 < S; s0 += 8) {
+                            float ms[8];
+#pragma unroll
+                            for (int u = 0; u < 8; u++) ms[u] = s0 + u < S ? ld_sc1(p0 + (s0 + u) * kPartStride) : -INFINITY;
+#pragma unroll
+                            for (int u = 0; u < 8; u++) mx = fmaxf(mx, ms[u]);
+                        }
+                        float Lsum = 0.0f, o = 0.0f;
+                        for (int s0 = 0; s0 < S; s0 += 8) {
+                            float ms[8], ls[8], os[8];
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                const float* ps = p0 + min(s0 + u, S - 1) * kPartStride;
+                                ms[u] = ld_sc1(ps);
+                                ls[u] = ld_sc1(ps + 1);
+                                os[u] = ld_sc1(ps + 4 + tid);
+                            }
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                const float wgt = (s0 + u < S && ms[u] != -INFINITY) ? __expf(ms[u] - mx) : 0.0f;
+                                Lsum += wgt * ls[u];
+                                o += wgt * os[u];
+                            }
+                        }
+                        res[tid] = o * (1.0f / Lsum);
+                    }
+                    __syncthreads();
+                    if (tid < 32) put_g(g_xo, (long)m * (D / 2) + h * 32 + tid, tag(l, 5), pack2<T>(res[2 * tid], res[2 * tid + 1]));
+                }
+                stamp(l, 4, 1);
+            }
+        }
+        // ---- F: cross-out projection + residual -------------------------------------------------------------------
+        {
+            if (!sweep_xs(g_xo, D / 2, tag(l, 5))) return;
+            stamp(l, 5, 0);
+            float acc[NC1][MAXM];
+            wxo.template run<MAXM>(xs, D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NC1; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wxo.nc && lane == m) {
+                        const int n = wxo.c0 + cl;
+                        xcur[j][m] = (acc[j][m] + W.bxo[n]) + xcur[j][m];
+                        put_g(g_x2, (long)m * D + n, tag(l, 6), __builtin_bit_cast(uint32_t, xcur[j][m]));
+                    }
+                }
+            stamp(l, 5, 1);
+        }
+        // ---- G: LN + FC1 + GELU (ggml's f16 table; rounded to T) ----------------------------------------------
+        {
+            wf2.load(W.f2, D, 4 * D, false);
+            if (!sweep_xf(g_x2, tag(l, 6))) return;
+            stamp(l, 6, 0);
+            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs);
+            __syncthreads();
+            float acc[NC4][MAXM];
+            wf1.template run<MAXM>(xs, D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NC4; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wf1.nc && lane == m) {
+                        const int n = wf1.c0 + cl;
+                        ost[m * CMAX + cl] = (float)(T)gelu_t(acc[j][m] + W.b1[n], a.gelu_tab);
+                    }
+                }
+            publish_pairs(g_ff, 2 * D, wf1.c0, wf1.nc, tag(l, 7));
+            stamp(l, 6, 1);
+        }
+        // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
+        {
+            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, 3 * D, D, true);
+            if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
+            stamp(l, 7, 0);
+            float acc[NC1][MAXM];
+            wf2.template run<MAXM>(xs, 4 * D, M, acc);
+#pragma unroll
+            for (int j = 0; j < NC1; j++)
+#pragma unroll
+                for (int m = 0; m < MAXM; m++) {
+                    const int cl = wave + 4 * j;
+                    if (m < M && cl < wf2.nc && lane == m) {
+                        const int n = wf2.c0 + cl;
+                        xcur[j][m] = (acc[j][m] + W.b2[n]) + xcur[j][m];
+                        put_g(g_x0, (long)m * D + n, tag(l + 1, 0), __builtin_bit_cast(uint32_t, xcur[j][m]));
+                    }
+                }
+            stamp(l, 7, 1);
+        }
+    }
+    // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
+    if (w0 == 0) {
+        if (!sweep_xf(g_x0, tag(L, 0))) return;
+        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh);
+    }
+}
+
+// one launcher per (compute type, weight form); the GGML-block form is built for the catalog's quantized
+// shapes (small 768, medium 1024, large-v3 1280)
+template <typename T, bool Q>
+void pdec_launch_t(const PdecArgs& a, size_t lds, hipStream_t st) {
+#define WM_PD(DD)                                                        \
+    case DD:                                                            \
+        pdec_kernel<T, DD, kPdecMaxRows, Q><<<kG, kNT, lds, st>>>(a);   \
+        return;
+    if constexpr (!Q) {
+        switch (a.d) { WM_PD(384) WM_PD(512) default: break; }
+    }
+    switch (a.d) { WM_PD(768) WM_PD(1024) WM_PD(1280) default: break; }
+#undef WM_PD
+    WM_FAIL("pdec: d %d%s", a.d, Q ? " (GGML blocks)" : "");
+}
+
+}  // namespace wm

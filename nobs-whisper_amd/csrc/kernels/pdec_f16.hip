@@ -1,0 +1,6 @@
+// Persistent decode step, half_t plain weights (one translation unit per instantiation set: they build in parallel)
+#include "pdec_body.h"
+
+namespace wm {
+void pdec_launch_f16(const PdecArgs& a, size_t lds, hipStream_t st) { pdec_launch_t<half_t, false>(a, lds, st); }
+}  // namespace wm

@@ -60,6 +60,7 @@ def test_over_256_clips_equal_smaller_batches_and_oracle(wrs, monkeypatch):
     from conftest import model_path
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
     monkeypatch.setenv("WHISPER_MI355X_SMALLM", "0")  # tail steps of few active clips: the split-K path too
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")  # and no persistent step (its key splits follow the clip count)
     monkeypatch.setenv("WHISPER_MI355X_XWIDE_MAX", "0")  # the 256-thread cross step at every clip count
     path = model_path("tiny+conf")
     n = 260
@@ -90,6 +91,7 @@ def test_turbo_bf16_256_equals_two_128(wrs, monkeypatch):
     from conftest import model_path
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
     monkeypatch.setenv("WHISPER_MI355X_SMALLM", "0")  # tail steps of few active clips: the split-K path too
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")  # and no persistent step (its key splits follow the clip count)
     monkeypatch.setenv("WHISPER_MI355X_XWIDE_MAX", "0")  # the 256-thread cross step at every clip count
     path = model_path("large-v3-turbo-2L+conf")
     clips = [synthetic_pcm(k % 32, seconds=30.0 - 0.5 * (k // 32)) for k in range(256)]

@@ -278,6 +278,7 @@ def test_small_bf16_batch32_equals_single(wrs, monkeypatch):
     from conftest import model_path
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
     monkeypatch.setenv("WHISPER_MI355X_SMALLM", "0")  # one decode path for batch and single (the small-M
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")  # and no persistent step (its key splits follow the clip count)
     monkeypatch.setenv("WHISPER_MI355X_XWIDE_MAX", "0")  # the 256-thread cross step at every clip count
     # path of <= 4 active clips sums in another order)
     path = model_path("small-4L+conf")

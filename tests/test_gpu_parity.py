@@ -156,9 +156,10 @@ def test_fixed_work_mode_matches_oracle(wrs, tiny_model):
     st.close(); ctx.close(); o.close()
 
 
-def test_batch_equals_single(wrs, tiny_model):
+def test_batch_equals_single(wrs, tiny_model, monkeypatch):
     """whisper_mi355x_full_batch over 4 clips (one of them 12 s) == 4 whisper_full_with_state calls
-    on fresh states."""
+    on fresh states (the per-kernel path: the persistent step's key splits follow the clip count)."""
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")
     ctx = wrs.WhisperContext(tiny_model, dtype=wrs.F16)
     clips = [synthetic_pcm(k) for k in range(3)] + [synthetic_pcm(7, seconds=12.0)]
     p = wrs.reference_full_params("en")

@@ -6,6 +6,8 @@ cross K/V cache form.
     oracle on every model width the kernel is built for (d 384 / 512 / 768 / 1280; 1024 is in
     tests/test_gpu_fulldepth.py), with the reference's FullParams, prompted and auto-language cases
     (a clip with an oracle near tie <= F16_GAP nats: identical up to that step);
+  * GGML-block files (the app's catalog: small-q5_1, medium-q5_0, large-v3-q5_0; plus q4_1 / q8_0) through
+    the block-streaming kernel (f16 compute): exact against the oracle like the f16 cases;
   * a batch of 4 clips (the largest it takes) against the oracle clip by clip;
   * the give-up path: with a zero spin limit every launch gives up and the step is re-run on the
     per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit;
@@ -98,6 +100,15 @@ def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
         k = assert_diverges_only_at_close_calls(got, exp, margins, F16_GAP, 4)
         print(f"{shape} clip {clip}: {n} persistent steps, {k} of {len(exp)} tokens identical "
               f"(oracle near tie {min(margins):.4f} nats)")
+
+
+QUANT_CASES = [("small-4L+conf+q5_1", 1, "en", None, 0.2), ("large-v3-2L+conf+q5_0", 0, "en", None, 0.2),
+               ("large-v3-turbo-2L+conf+q4_1", 1, "en", None, 0.2), ("large-v3-2L+conf+q8_0", 1, None, None, 0.2)]
+
+
+@pytest.mark.parametrize("shape,clip,lang,prompt,t_inc", QUANT_CASES)
+def test_pdec_quant_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc):
+    test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
 
 
 def test_pdec_batch4_vs_oracle(wrs, monkeypatch):

@@ -143,6 +143,7 @@ def test_quant_batch_equals_single(wrs, monkeypatch, shape):
     from test_gpu_configs import seg_ints
     monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
     monkeypatch.setenv("WHISPER_MI355X_QSMALL_MAX", "64")
+    monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")  # singles on the small-M path too
     monkeypatch.setenv("WHISPER_MI355X_XWIDE_MAX", "0")  # the 256-thread cross step at every clip count
     ctx = wrs.WhisperContext(model_path(shape), dtype=wrs.F16)
     clips = [synthetic_pcm(k % 12, seconds=30.0 - k % 5) for k in range(40)]

@@ -1,10 +1,10 @@
 """Per-phase timeline of the persistent decode step (kernels/pdec.hip) from its debug clock stamps.
 
 Every workgroup writes the 100 MHz clock when a phase's input arrived (its wait returned) and when it
-signalled the phase done; the last captured step's stamps are summarised per phase over the layers:
-  work    median over WGs of (signal - input)            the phase's own compute + payload drain
-  skew    max - min over WGs of the signal time           load imbalance / stragglers
-  hand    min over WGs of the next input - max signal     counter hand-off latency (last arrival -> first wake)
+published its output; the last captured step's stamps are summarised per phase over the layers:
+  work    median over WGs of (publish - input)            the phase's own compute
+  skew    max - min over WGs of the publish time          load imbalance / stragglers
+  hand    min over WGs of the next input - max publish    hand-off latency (last producer -> first consumer)
 usage: python tools/pdec_stamps.py [shape] [dtype] [clips] [steps]
 """
 import ctypes as C
@@ -45,23 +45,25 @@ def main():
     if not s.any():
         print("no stamps (persistent path not taken?)")
         return 1
-    t0 = s[:, 0, 0, 0].min()
+    s[s == 0] = np.nan  # the attention phases stamp only the workgroups that hold a task
+    t0 = np.nanmin(s[:, 0, 0, 0])
     s -= t0
-    tot = s[:, nl - 1, 7, 1].max()
+    tot = np.nanmax(s[:, nl - 1, 7, 1])
     print(f"{shape} {dtype} {n_clips} clip(s): step {tot / 1e3:.1f} us over {nl} layers ({tot / nl / 1e3:.2f} us/layer)")
     print(f"{'phase':12s} {'work us':>8s} {'skew us':>8s} {'hand us':>8s} {'first-in':>9s} {'last-sig':>9s}")
     sums = np.zeros(3)
     for p in range(8):
-        work = np.median(s[:, :, p, 1] - s[:, :, p, 0], axis=0)
-        skew = s[:, :, p, 1].max(axis=0) - s[:, :, p, 1].min(axis=0)
+        work = np.nanmedian(s[:, :, p, 1] - s[:, :, p, 0], axis=0)
+        skew = np.nanmax(s[:, :, p, 1], axis=0) - np.nanmin(s[:, :, p, 1], axis=0)
         if p < 7:
             nxt = s[:, :, p + 1, 0]
         else:
             nxt = np.concatenate([s[:, 1:, 0, 0], np.full((256, 1), np.nan)], axis=1)
-        hand = np.nanmin(nxt, axis=0) - s[:, :, p, 1].max(axis=0)
-        w, k, h = work.mean() / 1e3, skew.mean() / 1e3, np.nanmean(hand) / 1e3
+        with np.errstate(all="ignore"):
+            hand = np.nanmin(nxt, axis=0) - np.nanmax(s[:, :, p, 1], axis=0)
+        w, k, h = np.nanmean(work) / 1e3, np.nanmean(skew) / 1e3, np.nanmean(hand) / 1e3
         sums += (w, k, h)
-        print(f"{PHASES[p]:12s} {w:8.2f} {k:8.2f} {h:8.2f} {s[:, 1, p, 0].min() / 1e3:9.2f} {s[:, 1, p, 1].max() / 1e3:9.2f}")
+        print(f"{PHASES[p]:12s} {w:8.2f} {k:8.2f} {h:8.2f} {np.nanmin(s[:, 1, p, 0]) / 1e3:9.2f} {np.nanmax(s[:, 1, p, 1]) / 1e3:9.2f}")
     print(f"{'sum':12s} {sums[0]:8.2f} {sums[1]:8.2f} {sums[2]:8.2f}   (layer 1 absolute times in the last columns)")
     st.close()
     ctx.close()
