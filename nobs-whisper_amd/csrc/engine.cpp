@@ -602,16 +602,16 @@ static void tgemm_fp8(whisper_state* s, int epi, const GemmArgs& g, const float*
 static int enc_gelu_epi(DType dt) { return dt == DType::BF16 ? EPI_GELU_F : EPI_GELU; }
 
 // Projection weights of one layer in the compute type: the arena's matrices, or, for a block-quantized
-// file, the layer's blocks dequantized into the state's scratch (one layer at a time, on the stream
-// that then runs the layer: the encoder and the prefill are big-M GEMMs that read every weight many
-// times, so they read a dequantized copy; decode steps read the blocks themselves, gemm_small_kernel)
-struct LayerMats { const void *wqkv, *wo, *wxq, *wxo, *w1, *w2; };
-static LayerMats layer_mats(Context* c, whisper_state* s, const LayerW& L, hipStream_t st) {
-    LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
-    if (!c->quant) return m;
+// file, the context's expanded copy (ensure_expanded: every projection dequantized once per context,
+// 3.2 GB for large-v3, on first use outside a graph capture). The encoder, the prefill and the decode
+// steps of many clips are big-M GEMMs that read every weight many times, so they read the copy; the
+// decode steps of few clips stream the blocks themselves (gemm_small_kernel, the persistent step).
+// Until the copy exists (a first use inside a capture) a layer is dequantized into the state's scratch.
+using LayerMats = Context::LayerMats;
+// (returns the end of the layer's matrices in p)
+static char* dequant_layer(Context* c, const LayerW& L, char* p, LayerMats& m, hipStream_t st) {
     const int d = c->hp.n_audio_state;
     const size_t E = esize(c->dt);
-    char* p = (char*)s->ws.wdq;
     // one launch for the layer when its blocks share one type (a ggml file quantizes every projection
     // alike), else one per matrix
     DequantJobs J;
@@ -632,6 +632,41 @@ static LayerMats layer_mats(Context* c, whisper_state* s, const LayerW& L, hipSt
     if (one_type) launch_dequant_multi(c->dt, J, st);
     else
         for (int j = 0; j < J.n; j++) launch_dequant(c->dt, J.q[j], J.rows[j], J.K[j], J.out[j], st);
+    return p;
+}
+
+static void ensure_expanded(Context* c, hipStream_t st) {
+    if (!c->quant || c->expanded.load(std::memory_order_acquire)) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    WM_CHECK(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) return;
+    std::lock_guard<std::mutex> lk(c->exp_mu);
+    if (c->expanded.load(std::memory_order_relaxed)) return;
+    // encoder layers: QKV, out, FC1, FC2 = 12 d^2; decoder layers + cross Q, cross out = 14 d^2
+    const size_t d = c->hp.n_audio_state;
+    dalloc(c->arena_exp, (12 * c->w.enc.size() + 14 * c->w.dec.size()) * d * d * esize(c->dt));
+    char* p = c->arena_exp;
+    auto fill = [&](const std::vector<LayerW>& layers, std::vector<LayerMats>& out) {
+        out.resize(layers.size());
+        for (size_t l = 0; l < layers.size(); l++) {
+            const LayerW& L = layers[l];
+            out[l] = LayerMats{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
+            p = dequant_layer(c, L, p, out[l], st);
+        }
+    };
+    fill(c->w.enc, c->exp_enc);
+    fill(c->w.dec, c->exp_dec);
+    WM_CHECK(hipStreamSynchronize(st));  // other states' streams read the copy from now on
+    c->expanded.store(true, std::memory_order_release);
+}
+
+static LayerMats layer_mats(Context* c, whisper_state* s, bool dec, int l, hipStream_t st) {
+    const LayerW& L = dec ? c->w.dec[l] : c->w.enc[l];
+    LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
+    if (!c->quant) return m;
+    ensure_expanded(c, st);
+    if (c->expanded.load(std::memory_order_acquire)) return dec ? c->exp_dec[l] : c->exp_enc[l];
+    dequant_layer(c, L, (char*)s->ws.wdq, m, st);
     return m;
 }
 
@@ -689,7 +724,7 @@ int encode_windows(Context* c, whisper_state* s, const int* jobs, const int* see
                 tgemm_fp8(s, EPI_RESID, gemm_plain(w.qkv, M, 4 * d, F.w2, d, L.b2, w.x, d), w.hs, F.s2, st);
                 continue;
             }
-            const LayerMats Wm = layer_mats(c, s, L, st);
+            const LayerMats Wm = layer_mats(c, s, false, l, st);
             launch_layernorm(dt, w.x, nullptr, M, d, L.ln1_w, L.ln1_b, w.hn, st);
             tgemm(s, KCLS, dt, EPI_STORE, gemm_plain(w.hn, M, d, Wm.wqkv, 3 * d, L.bqkv, w.qkv, 3 * d), st);
             {
@@ -1072,7 +1107,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         const int lw = l;
         LayerW Lw = W.dec[lw];
         if (c->quant) {  // prefill / language detection: this layer's blocks dequantized into the scratch
-            const LayerMats m = layer_mats(c, s, Lw, st);
+            const LayerMats m = layer_mats(c, s, true, lw, st);
             Lw.wqkv = (void*)m.wqkv; Lw.wo = (void*)m.wo; Lw.wxq = (void*)m.wxq; Lw.wxo = (void*)m.wxo;
             Lw.w1 = (void*)m.w1; Lw.w2 = (void*)m.w2;
         }
@@ -1182,9 +1217,9 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
     const int gsz = cdiv(n_tok, groups);
     DecView half[2];
     dec_halves(c, s, gsz, xdirect, half[0], half[1]);
-    // block-quantized files: one dequantization scratch per state, so the groups run one after the
-    // other on the state's stream
-    if (c->quant) half[1] = half[0];
+    // block-quantized files before the expanded copy exists: one dequantization scratch per state, so
+    // the groups run one after the other on the state's stream
+    if (c->quant && !c->expanded.load(std::memory_order_acquire)) half[1] = half[0];
     WM_CHECK(hipEventRecord(s->ev_fork, s->stream));
     WM_CHECK(hipStreamWaitEvent(s->stream2, s->ev_fork, 0));
     for (int g = 0, r0 = 0; r0 < n_tok; g++, r0 += gsz) {
@@ -1700,6 +1735,7 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
         if (!warned) fprintf(stderr, "whisper_mi355x: greedy best_of=%d: fallback attempts sample 1 candidate\n", p.greedy.best_of);
         warned = true;
     }
+    ensure_expanded(c, s->stream);  // quantized files: before anything is captured
     Sched S;
     S.c = c; S.s = s; S.p = p; S.o = o; S.single_api = single_api;
     const Vocab& v = c->vocab;

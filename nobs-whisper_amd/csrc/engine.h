@@ -2,6 +2,7 @@
 // and the batched window scheduler that implements whisper_full semantics for many clips at once.
 #pragma once
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <random>
 #include <string>
@@ -85,9 +86,15 @@ struct Context {
     // model (its per-head transposed Wk is in the arena); each call picks direct or cached form.
     bool cross_direct = false;
     // block-quantized file (ggml type of its projection matrices, 0 = f16/f32 file) kept quantized in
-    // the arena: decode steps read the blocks (gemm_small_kernel), the encoder and prefill dequantize
-    // one layer at a time into the state's scratch
+    // the arena: decode steps of few clips read the blocks (gemm_small_kernel, the persistent step);
+    // the big-M GEMMs (encoder, prefill, decode steps of many clips) read a compute-type copy of every
+    // projection, expanded once per context on first use (ensure_expanded, engine.cpp)
     int quant = 0;
+    struct LayerMats { const void *wqkv, *wo, *wxq, *wxo, *w1, *w2; };
+    std::mutex exp_mu;
+    std::atomic<bool> expanded{false};
+    char* arena_exp = nullptr;
+    std::vector<LayerMats> exp_enc, exp_dec;
     std::string model_type;
     whisper_context* owner = nullptr;  // the whisper.h handle wrapping this context
     // fp8 encoder (large-v3-turbo fp8 config): QKV, FC1 and FC2 as e4m3 GEMMs with per-row scales.

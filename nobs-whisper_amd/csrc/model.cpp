@@ -503,6 +503,7 @@ bool load_context(Context* c, const char* path, int device, DType dt, bool load_
 void free_context(Context* c) {
     if (c && c->arena) { hipSetDevice(c->device); hipFree(c->arena); c->arena = nullptr; }
     if (c && c->arena8) { hipSetDevice(c->device); hipFree(c->arena8); c->arena8 = nullptr; }
+    if (c && c->arena_exp) { hipSetDevice(c->device); hipFree(c->arena_exp); c->arena_exp = nullptr; }
     if (c && c->pdec_layers) { hipSetDevice(c->device); hipFree(c->pdec_layers); c->pdec_layers = nullptr; }
 }
 

@@ -150,3 +150,40 @@ def test_state_outliving_its_context(wrs):
     st = ctx2.create_state()
     ctx2.close()
     assert st.ptr is None
+
+
+def test_cross_cache_regrow_drops_stale_graphs(wrs, monkeypatch):
+    """one state runs a direct-form batch of 40 clips (workspace for 64 slots, no cross
+    K/V cache), then cache-form batches of 8 clips (decode graphs captured for <= 8 active clips over
+    the cache) and 16 clips (the cache is reallocated larger). The 8-clip batch run again after the
+    reallocation replays graphs for <= 8 clips: they must have been dropped with the old cache, so every
+    result equals a fresh state's, bit for bit."""
+    from conftest import model_path
+    path = model_path("tiny+conf")
+    p = wrs.reference_full_params("en")
+    p.temperature_inc = 0.0
+    clips = [synthetic_pcm(k % 12, seconds=30.0 - k % 5) for k in range(40)]
+
+    def run(st, cl):
+        assert st.full_batch(p, cl) == 0
+        return [seg_ints(st.batch_segments(j)) for j in range(len(cl))]
+
+    monkeypatch.setenv("WHISPER_MI355X_STATE_POOL", "0")  # every state starts with no workspace
+    ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    fresh = {}
+    for key, cl in (("a", clips[:8]), ("b", clips[8:24])):
+        s = ctx.create_state()
+        fresh[key] = run(s, cl)
+        s.close()
+    st = ctx.create_state()
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "direct")
+    run(st, clips)
+    assert st.info()["direct"]
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    assert run(st, clips[:8]) == fresh["a"]
+    assert not st.info()["direct"]
+    assert run(st, clips[8:24]) == fresh["b"]
+    assert run(st, clips[:8]) == fresh["a"]
+    st.close()
+    ctx.close()
