@@ -161,7 +161,7 @@ def cpu_baseline(model_path: str, threads: int, n_tokens: int, n_sample_tokens: 
 # cross-attention form for the decode-step class: straight from the encoder output, or the cached K/V
 K_SYMBOL = {("gemm_encoder", None): r"gemm8p_kernel", ("attn_encoder", None): r"attn_enc2_kernel",
             ("attn_cross_decode", True): r"xattn_step_kernel",
-            ("attn_cross_decode", False): r"attn_cross_step_(wide_)?kernel"}
+            ("attn_cross_decode", False): r"attn_cross_step_(wide_)?kernel", ("pdec_step", None): r"pdec_kernel"}
 
 
 def cross_step_grid(direct: bool, nb: int, heads: int, wide_max: int = 4) -> int:
@@ -662,6 +662,8 @@ def main():
         if K_NAMES[dom] == "attn_cross_decode":
             from make_model import SHAPES
             grid = cross_step_grid(bool(form["direct"]), nb, SHAPES[args.model][3])
+        elif K_NAMES[dom] == "pdec_step":
+            grid = 256 * 256  # one 256-thread workgroup per CU, whatever the clip count
         traffic, src = pmc_traffic(K_NAMES[dom], form["direct"], grid)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

@@ -497,12 +497,15 @@ int compute_mel(Context* c, whisper_state* s, const float* const* pcm, const int
         ints[j] = n[j];
         ints[n_jobs + j] = mel_n_len(n[j]);
     }
-    // one host block -> device: [mel ptrs][pcm ptrs][n][n_len][max]
-    std::vector<char> blk(n_jobs * (2 * sizeof(void*) + 3 * sizeof(int)));
+    // one host block -> device, laid out as the workspace carves it (ensure_ws: arrays of cap_jobs
+    // entries, whatever this call's clip count): [mel ptrs][pcm ptrs][n][n_len] ([max] is the kernel's)
+    const size_t cap = w.cap_jobs;
+    std::vector<char> blk(cap * (2 * sizeof(void*) + 2 * sizeof(int)));
     memcpy(blk.data(), mp.data(), n_jobs * sizeof(void*));
-    memcpy(blk.data() + n_jobs * sizeof(void*), pp.data(), n_jobs * sizeof(void*));
-    memcpy(blk.data() + 2 * n_jobs * sizeof(void*), ints.data(), 2 * n_jobs * sizeof(int));
-    WM_CHECK(hipMemcpyAsync(w.mel_ptrs, blk.data(), blk.size() - n_jobs * sizeof(int), hipMemcpyHostToDevice, s->stream));
+    memcpy(blk.data() + cap * sizeof(void*), pp.data(), n_jobs * sizeof(void*));
+    memcpy(blk.data() + 2 * cap * sizeof(void*), ints.data(), n_jobs * sizeof(int));
+    memcpy(blk.data() + 2 * cap * sizeof(void*) + cap * sizeof(int), ints.data() + n_jobs, n_jobs * sizeof(int));
+    WM_CHECK(hipMemcpyAsync(w.mel_ptrs, blk.data(), blk.size(), hipMemcpyHostToDevice, s->stream));
     {
         double bytes = 0;
         for (int j = 0; j < n_jobs; j++)

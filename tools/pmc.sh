@@ -7,8 +7,8 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
 # BATCHES: one pass pair per global batch (the strong-scaling shards: 128 / 64 / 32 / 16 clips per GPU
 # at 1 / 2 / 4 / 8 GPUs; up to 32 clips the cached cross form runs attn_cross_step_kernel)
-ARGS="--tokens 4 --steps 1 --warmup 1 --cpu-baseline 0 --variants 0 --frontend 0 --app-pattern 0"
-REGEX="${PMC_REGEX:-xattn_step_kernel|attn_cross_step_kernel|gemm8p_kernel|attn_enc2_kernel}"
+ARGS="--tokens 4 --steps 1 --warmup 1 --cpu-baseline 0 --variants 0 --frontend 0 --app-pattern 0 ${PMC_ARGS}"
+REGEX="${PMC_REGEX:-xattn_step_kernel|attn_cross_step|gemm8p_kernel|attn_enc2_kernel|gemm_dec_kernel|splitk_reduce|pdec_kernel|gemm_small_kernel}"
 for B in ${BATCHES:-128}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     d="$R/gpurun_out/pmc_$(echo $c | tr A-Z a-z | cut -d_ -f1)_b$B"
