@@ -325,13 +325,12 @@ template <typename T>
 __device__ __forceinline__ T hi_t(uint32_t v) { return __builtin_bit_cast(T, (uint16_t)(v >> 16)); }
 
 // The workgroup waits for granules addr(0 .. n-1) of g to carry `tag` (every thread its own i = tid + kNT u,
-// 8 loads in flight per pass) and hands each granule's data to put(i, bits). A thread gives up after
+// U loads in flight per pass) and hands each granule's data to put(i, bits). A thread gives up after
 // spin_ticks (100 MHz) or when another workgroup set the error word; false = give up (the caller returns,
 // so every workgroup drains).
-template <typename A, typename P>
+template <int U = 8, typename A, typename P>
 __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsigned tag, A addr, P put, unsigned* err,
                                       int* lflag, long spin_ticks) {
-    constexpr int U = 8;
     bool ok = true;
     for (int b = 0; b < n && ok; b += kNT * U) {
         unsigned long long v[U];
@@ -522,8 +521,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     auto sweep_xf = [&](unsigned long long* g, unsigned tg) {
         return sweep(g, M * D, tg, [](int i) { return (long)i; }, [&](int i, uint32_t b) { xf[i] = f32_of(b); }, err, lflag, spin);
     };
-    auto sweep_xs = [&](unsigned long long* g, int nw, unsigned tg) {
-        return sweep(g, M * nw, tg, [](int i) { return (long)i; },
+    auto sweep_xs = [&](unsigned long long* g, int nw, unsigned tg) {  // (the GELU rows: 2d granules per row)
+        return sweep<16>(g, M * nw, tg, [](int i) { return (long)i; },
                      [&](int i, uint32_t b) { xs[2 * i] = lo_t<T>(b); xs[2 * i + 1] = hi_t<T>(b); }, err, lflag, spin);
     };
     // packed outputs: lane m of wave w holds column c0 + w + 4 j of row m; staged in LDS, then one granule per pair
