@@ -291,7 +291,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd); dfree(w.pd_sync);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync);
     if (w.h_pd_err) hipHostFree(w.h_pd_err);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
@@ -888,9 +888,8 @@ static const PdecLayer* pdec_layers(Context* c) {
 static void pdec_prepare(Context* c, whisper_state* s) {
     Workspace& w = s->ws;
     pdec_layers(c);
-    if (w.pd) return;
-    // the cross-attention partials; the hand-off block
-    dalloc(w.pd, (size_t)256 * 68 * sizeof(float));
+    if (w.pd_sync) return;
+    // the hand-off block
     dalloc(w.pd_sync, pdec_granules(c->hp.n_text_state, c->hp.n_text_layer, c->hp.n_text_head).bytes);
     WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
     *w.h_pd_err = 0;
@@ -905,7 +904,7 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab;
     const int n = v.n;
     hipStream_t st = v.st;
-    if (!w.pd || !c->pdec_layers) WM_FAIL("pdec: buffers not allocated (pdec_prepare)");
+    if (!w.pd_sync || !c->pdec_layers) WM_FAIL("pdec: buffers not allocated (pdec_prepare)");
     PdecArgs a{};
     a.layers = (const PdecLayer*)c->pdec_layers;
     a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.n_audio_ctx = hp.n_audio_ctx;
@@ -916,7 +915,6 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
     a.self_cache = w.self; a.cross_cache = w.cross;
     a.k_scale = c->k_scale;
-    a.xpart = w.pd;
     a.quant = c->w.dec[0].qqkv.type != 0;
     a.s_cross = pdec_cross_splits(n, H, hp.n_audio_ctx);
     a.sync = w.pd_sync;

@@ -168,8 +168,7 @@ struct Workspace {
     TokOut* tout = nullptr;
     void* lrec = nullptr;  // split logits kernel: per-chunk records
     int *win_job = nullptr, *win_seek = nullptr, *win_slot = nullptr;
-    // persistent decode step: in-launch hand-off buffers, counters, and the error word's host copy
-    float* pd = nullptr;
+    // persistent decode step: the hand-off block (granules + error word) and the error word's host copy
     unsigned* pd_sync = nullptr;
     unsigned* h_pd_err = nullptr;
     // mel / pcm

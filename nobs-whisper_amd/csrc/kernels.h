@@ -193,11 +193,12 @@ struct PdecLayer {
 };
 // The hand-off block (one allocation, zeroed before every launch): data-tagged 8-byte granules (offsets
 // in granules): x rows x0, x1, x2 [R][d] (f32), and packed T pairs: qkv [R][3d/2], self-attention output
-// so [R][d/2], cross q qx [R][d/2], cross-attention output xo [R][d/2], GELU rows ff [R][2d]; then the
-// cross-attention merge tickets [L][R][H] (u32) and the error word (byte offsets); R = kPdecMaxRows.
+// so [R][d/2], cross q qx [R][d/2], cross-attention output xo [R][d/2], GELU rows ff [R][2d]; the
+// cross-attention split partials part [256][66] (f32: o[64], max, sum); then the error word (byte
+// offset); R = kPdecMaxRows.
 struct PdecGranules {
-    long x0, x1, x2, qkv, so, qx, xo, ff;
-    long tick_bytes, err_bytes, bytes;
+    long x0, x1, x2, qkv, so, qx, xo, ff, part;
+    long err_bytes, bytes;
 };
 PdecGranules pdec_granules(int d, int L, int H);
 struct PdecArgs {
@@ -208,7 +209,6 @@ struct PdecArgs {
     const int *tok, *pos, *slot;      // [M]
     void* self_cache; const void* cross_cache;
     float k_scale;
-    float* xpart;                       // cross-attention partials [M * H * s_cross][68] (f32)
     int s_cross;                        // key splits per (clip, head) of the cross attention
     int quant;                          // the layers' matrices are GGML blocks (PdecMat.qt != 0)
     void* sync;                         // the hand-off block (gr.bytes), zeroed by the launcher

@@ -57,27 +57,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kG = 256;         // workgroups = CUs (one per CU)
 constexpr int kNT = 256;        // threads per workgroup
 constexpr int kPhases = 8;
-constexpr int kPartStride = 68; // floats per attention partial: m, l, pad x2, o[64]
+constexpr int kPartG = 66;      // granules per cross-attention partial: o[64], max, sum
 enum { P_X0 = 0, P_QKV, P_SELF, P_X1, P_XQ, P_XATT, P_X2, P_FF };
 
 // global (not flat) address space for the plain loads: flat loads also count in lgkmcnt
 template <typename P>
 __device__ __forceinline__ const __attribute__((address_space(1))) P* gp(const P* p) {
     return (const __attribute__((address_space(1))) P*)p;
-}
-
-__device__ __forceinline__ float ld_sc1(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 0x7fffffff, 0x00020000);
-}
-// 16-byte sc1 load / store of a buffer written inside this launch (aux 16 = sc1)
-__device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
-    return __builtin_bit_cast(float4, v);
-}
-__device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, float4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16);
 }
 
 template <int CTRL>
@@ -259,44 +245,55 @@ struct ColSlice {
     }
 };
 
-// LayerNorm of rows [0, M) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global): one wave per
-// row, layernorm_kernel's arithmetic (double sums, separately rounded ops)
+// LayerNorm of rows [0, M) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
+// layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over wpr = 4 / M
+// waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
+// per row. The row is re-read from LDS in each pass (no register copy: the weights of the next phases
+// are held in registers meanwhile).
 template <typename T, int D>
-__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __restrict__ w, const float* __restrict__ b, T* out) {
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __restrict__ w, const float* __restrict__ b, T* out,
+                                        double* lred) {
 #pragma clang fp contract(off)
-    constexpr int NPL = (D + 63) / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int m = wave; m < M; m += 4) {
-        float v[NPL];
-#pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * e;
-            v[e] = k < D ? xf[m * D + k] : 0.0f;
-        }
+    const int wpr = M == 1 ? 4 : (M == 2 ? 2 : 1);  // uniform
+    const int nrow = M < 3 ? M : 4;                  // rows handled at once
+    auto wsum = [](double x) {
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        return x;
+    };
+    for (int m0 = 0; m0 < M; m0 += nrow) {
+        const int m = m0 + wave / wpr, q = wave % wpr;
+        const bool on = m < M;
+        const float* x = xf + (long)m * D;
         double s = 0.0;
-#pragma unroll
-        for (int e = 0; e < NPL; e++) s += (double)v[e];
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        const float mean = (float)(s / D);
+        if (on)
+            for (int k = lane + 64 * q; k < D; k += 64 * wpr) s += (double)x[k];
+        s = wsum(s);
+        if (lane == 0) lred[wave] = s;
+        __syncthreads();
+        double st = 0.0;
+        for (int i = 0; i < wpr; i++) st += lred[(wave / wpr) * wpr + i];
+        const float mean = (float)(st / D);
         double s2 = 0.0;
-#pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * e;
-            v[e] = v[e] - mean;
-            if (k < D) s2 += (double)(v[e] * v[e]);
-        }
-        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
-        const float variance = (float)(s2 / D);
+        if (on)
+            for (int k = lane + 64 * q; k < D; k += 64 * wpr) {
+                const float v = x[k] - mean;
+                s2 += (double)(v * v);
+            }
+        s2 = wsum(s2);
+        if (lane == 0) lred[4 + wave] = s2;
+        __syncthreads();
+        double st2 = 0.0;
+        for (int i = 0; i < wpr; i++) st2 += lred[4 + (wave / wpr) * wpr + i];
+        const float variance = (float)(st2 / D);
         const float scale = 1.0f / sqrtf(variance + 1e-5f);
-#pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * e;
-            if (k < D) {
-                float t = v[e] * scale;
+        if (on)
+            for (int k = lane + 64 * q; k < D; k += 64 * wpr) {
+                float t = (x[k] - mean) * scale;
                 t = t * w[k];
                 out[(long)m * D + k] = (T)(t + b[k]);
             }
-        }
+        __syncthreads();  // lred is rewritten by the next rows / call
     }
 }
 
@@ -372,53 +369,58 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
     return r;
 }
 
-// One attention task: query q (64 f32 in LDS), keys/values rows [r0, r1) of (K, V) [rows][64] T, plus,
-// if fresh >= 0 and in range, row `fresh` taken from fk / fv (LDS f32) instead of the cache. Leaves in res
-// (LDS): o[64] = sum_t p_t v_t, res[64] = max score, res[65] = sum_t p_t, with p_t = e^(s_t - max)
-// (rounded to T as the P.V operand). 32 lane groups of 8 lanes, a key row per group and U rows in flight
-// per group; a range of at most one chunk (32 U rows) issues its V rows together with its K rows.
+// Attention over keys/values rows [r0, r1) of (K, V) [rows][64] T, at most 32 U rows (one chunk):
+// 32 lane groups of 8 lanes, a key row per group, U rows per group. attn_load issues every K and V row
+// load of the range into registers (rows from earlier launches: before the wait for this step's query);
+// row `fresh` (this position's k, v, handed off in this launch) is not loaded: attn_task takes it from
+// fk / fv (LDS f32). attn_task leaves in res (LDS): o[64] = sum_t p_t v_t, res[64] = max score,
+// res[65] = sum_t p_t, with p_t = e^(s_t - max) (rounded to T as the P.V operand).
 template <typename T, int U>
-__device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, int r0, int r1,
+__device__ __forceinline__ void attn_load(const T* __restrict__ K, const T* __restrict__ V, int r0, int r1, int fresh,
+                                          u32x4 (&rk)[U], u32x4 (&rv)[U]) {
+    const int lane8 = threadIdx.x & 7, grp = threadIdx.x >> 3;
+    constexpr int NG = kNT / 8;
+    const u32x4 zero = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int t = r0 + grp + NG * u;
+        const bool in = t < r1 && t != fresh;
+        rk[u] = in ? *gp((const u32x4*)(K + (long)t * 64 + lane8 * 8)) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int t = r0 + grp + NG * u;
+        const bool in = t < r1 && t != fresh;
+        rv[u] = in ? *gp((const u32x4*)(V + (long)t * 64 + lane8 * 8)) : zero;
+    }
+}
+template <typename T, int U>
+__device__ __forceinline__ void attn_task(const float* qs, const u32x4 (&rk)[U], const u32x4 (&rv)[U], int r0, int r1,
                                           int fresh, const float* fk, const float* fv, float* sc, float* red, float* res) {
     const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
-    constexpr int NG = kNT / 8, CH = NG * U;
-    const u32x4 zero = {0, 0, 0, 0};
+    constexpr int NG = kNT / 8;
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
-    auto load_rows = [&](const T* base, int t0, u32x4 (&raw)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + NG * u;
-            raw[u] = (t < r1 && t != fresh) ? *gp((const u32x4*)(base + (long)t * 64 + lane8 * 8)) : zero;
-        }
-    };
-    const bool one = r1 - r0 <= CH;
     float lmax = -INFINITY;
-    u32x4 rk[U], rv[U];
-    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
-        load_rows(K, t0, rk);
-        if (one) load_rows(V, t0, rv);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + NG * u;
-            const T* ke = (const T*)&rk[u];
-            float a = 0.0f;
-            if (t == fresh) {
+    for (int u = 0; u < U; u++) {
+        const int t = r0 + grp + NG * u;
+        const T* ke = (const T*)&rk[u];
+        float a = 0.0f;
+        if (t == fresh) {
 #pragma unroll
-                for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
-            } else {
+            for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
+        } else {
 #pragma unroll
-                for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-            }
-            a = sum8(a);
-            if (t < r1) {
-                if (lane8 == 0) sc[t - r0] = a;
-                lmax = fmaxf(lmax, a);
-            }
+            for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+        }
+        a = sum8(a);
+        if (t < r1) {
+            if (lane8 == 0) sc[t - r0] = a;
+            lmax = fmaxf(lmax, a);
         }
     }
-    if (!one) load_rows(V, r0 + grp, rv);  // the first V chunk lands under the softmax
     lmax = wave_max(lmax);
     if (lane == 0) red[wave] = lmax;
     __syncthreads();
@@ -435,12 +437,10 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
-    for (int t0 = r0 + grp; t0 < r1; t0 += CH) {
-        if (t0 != r0 + grp) load_rows(V, t0, rv);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + NG * u;
-            if (t >= r1) break;
+    for (int u = 0; u < U; u++) {
+        const int t = r0 + grp + NG * u;
+        if (t < r1) {
             const float p = sc[t - r0];
             if (t == fresh) {
 #pragma unroll
@@ -495,14 +495,15 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     float* qf = red + 8 + 256;                                        // q, fresh k, fresh v [3][64]
     float* res = qf + 192;                                            // attention result [64 + 2] (+ pad)
     float* ost = res + 68;                                            // packed outputs [M][CMAX]
-    int* lflag = (int*)(ost + MAXM * CMAX);
+    double* lred = (double*)(ost + MAXM * CMAX);                      // LayerNorm partial sums [8]
+    int* lflag = (int*)(lred + 8);
 
     const int M = a.M, L = a.L, w0 = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const PdecGranules& G = a.gr;
     unsigned long long* gb = (unsigned long long*)a.sync;
     unsigned long long *g_x0 = gb + G.x0, *g_x1 = gb + G.x1, *g_x2 = gb + G.x2, *g_qkv = gb + G.qkv;
     unsigned long long *g_so = gb + G.so, *g_qx = gb + G.qx, *g_xo = gb + G.xo, *g_ff = gb + G.ff;
-    unsigned* tick = (unsigned*)((char*)a.sync + G.tick_bytes);
+    unsigned long long* g_part = gb + G.part;
     unsigned* err = (unsigned*)((char*)a.sync + G.err_bytes);
     const T* te = (const T*)a.tok_emb;
     const float* te32 = a.te_f32 ? (const float*)a.tok_emb : nullptr;
@@ -568,7 +569,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 return;
             }
             stamp(l, 0, 0);
-            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs);
+            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs, lred);
             __syncthreads();
             float acc[NCQ][MAXM];
             wq.template run<MAXM>(xs, D, M, acc);
@@ -592,6 +593,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             wo.load(W.o, D, D, false);
             if (w0 < M * H) {
                 const int m = w0 / H, h = w0 % H;
+                const int pos = a.pos[m], nkv = pos + 1;
+                const long sl = a.slot[m];
+                T* Kc = (T*)self + (((sl * L + l) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
+                T* Vc = (T*)self + (((sl * L + l) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
+                u32x4 rk[16], rv[16];
+                attn_load<T, 16>(Kc, Vc, 0, nkv, pos, rk, rv);  // the cached rows land while the query is awaited
                 // q, k, v of head h: granules h * 32 + i of each third of the row
                 if (!sweep(g_qkv, 96, tag(l, 1), [&](int i) { return (long)m * (3 * D / 2) + (i >> 5) * (D / 2) + h * 32 + (i & 31); },
                            [&](int i, uint32_t b) {
@@ -600,15 +607,11 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 1, 0);
-                const int pos = a.pos[m], nkv = pos + 1;
-                const long sl = a.slot[m];
-                T* Kc = (T*)self + (((sl * L + l) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
-                T* Vc = (T*)self + (((sl * L + l) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
                 if (tid < 64) {  // append this position's k, v to the cache (read by the next steps' launches)
                     Kc[(long)pos * 64 + tid] = (T)qf[64 + tid];
                     Vc[(long)pos * 64 + tid] = (T)qf[128 + tid];
                 }
-                attn_task<T, 16>(qf, Kc, Vc, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
+                attn_task<T, 16>(qf, rk, rv, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
                 if (tid < 32) {
                     const float inv = 1.0f / res[65];
                     put_g(g_so, (long)m * (D / 2) + h * 32 + tid, tag(l, 2), pack2<T>(res[2 * tid] * inv, res[2 * tid + 1] * inv));
@@ -641,7 +644,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             wxo.load(W.xo, D, D, false);
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
-            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs);
+            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs, lred);
             __syncthreads();
             float acc[NCX][MAXM];
             wxq.template run<MAXM>(xs, D, M, acc);
@@ -658,12 +661,18 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             publish_pairs(g_qx, D / 2, wxq.c0, wxq.nc, tag(l, 4));
             stamp(l, 3, 1);
         }
-        // ---- E: cross attention over the cached K/V, split over keys; the last split of a (row, head) merges ----
+        // ---- E: cross attention over the cached K/V, split over keys; split 0 of a (row, head) merges -----------
         {
-            wf1.load(W.f1, 4 * D, D, true);
             const int S = a.s_cross;
             if (w0 < M * H * S) {
                 const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
+                const int T_ = a.n_audio_ctx;
+                const int r0 = (int)((long)s * T_ / S), r1 = (int)((long)(s + 1) * T_ / S);
+                const long sl = a.slot[m];
+                const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
+                const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
+                u32x4 rk[16], rv[16];
+                attn_load<T, 16>(Kc, Vc, r0, r1, -1, rk, rv);  // constant for the window: issued before the wait
                 if (!sweep(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
                            [&](int i, uint32_t b) {
                                qf[2 * i] = (float)lo_t<T>(b);
@@ -671,67 +680,40 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 4, 0);
-                const int T_ = a.n_audio_ctx;
-                const int r0 = (int)((long)s * T_ / S), r1 = (int)((long)(s + 1) * T_ / S);
-                const long sl = a.slot[m];
-                const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
-                const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
-                attn_task<T, 8>(qf, Kc, Vc, r0, r1, -1, nullptr, nullptr, sc, red, res);
-                // the partial {max, sum, 0, 0, o[64]}: sc1 stores, drained, then the (row, head) ticket
-                float* part = a.xpart + (long)w0 * kPartStride;
-                int* last = lflag + 1;
-                if (tid < 64) {
-                    st_sc1(part + 4 + tid, res[tid]);
-                    if (tid == 0) {
-                        st_sc1(part, res[64]);
-                        st_sc1(part + 1, res[65]);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                __syncthreads();
-                if (tid == 0)
-                    *last = __hip_atomic_fetch_add(tick + ((long)l * MAXM + m) * H + h, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
-                __syncthreads();
-                if (*last) {
-                    // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s over the S partials (sc1 loads)
-                    const float* p0 = a.xpart + (long)(w0 - s) * kPartStride;
+                attn_task<T, 16>(qf, rk, rv, r0, r1, -1, nullptr, nullptr, sc, red, res);
+                // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
+                // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
+                unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
+                if (s > 0) {
+                    if (tid < kPartG) put_g(gp0 + (long)s * kPartG, tid, tag(l, 4), __builtin_bit_cast(uint32_t, res[tid]));
+                } else {
+                    float* part = (float*)xs;  // [S][66] (xs is free until phase F's sweep)
+                    if (tid < kPartG) part[tid] = res[tid];
+                    if (!sweep<16>(gp0 + kPartG, (S - 1) * kPartG, tag(l, 4), [](int i) { return (long)i; },
+                                   [&](int i, uint32_t b) { part[kPartG + i] = f32_of(b); }, err, lflag, spin))
+                        return;
                     if (tid < 64) {
                         float mx = -INFINITY;
-                        for (int s0 = 0; s0 < S; s0 += 8) {
-                            float ms[8];
-#pragma unroll
-                            for (int u = 0; u < 8; u++) ms[u] = s0 + u < S ? ld_sc1(p0 + (s0 + u) * kPartStride) : -INFINITY;
-#pragma unroll
-                            for (int u = 0; u < 8; u++) mx = fmaxf(mx, ms[u]);
-                        }
+                        for (int u = 0; u < S; u++) mx = fmaxf(mx, part[u * kPartG + 64]);
                         float Lsum = 0.0f, o = 0.0f;
-                        for (int s0 = 0; s0 < S; s0 += 8) {
-                            float ms[8], ls[8], os[8];
-#pragma unroll
-                            for (int u = 0; u < 8; u++) {
-                                const float* ps = p0 + min(s0 + u, S - 1) * kPartStride;
-                                ms[u] = ld_sc1(ps);
-                                ls[u] = ld_sc1(ps + 1);
-                                os[u] = ld_sc1(ps + 4 + tid);
-                            }
-#pragma unroll
-                            for (int u = 0; u < 8; u++) {
-                                const float wgt = (s0 + u < S && ms[u] != -INFINITY) ? __expf(ms[u] - mx) : 0.0f;
-                                Lsum += wgt * ls[u];
-                                o += wgt * os[u];
-                            }
+                        for (int u = 0; u < S; u++) {
+                            const float ms = part[u * kPartG + 64];
+                            const float wgt = ms != -INFINITY ? __expf(ms - mx) : 0.0f;
+                            Lsum += wgt * part[u * kPartG + 65];
+                            o += wgt * part[u * kPartG + tid];
                         }
                         res[tid] = o * (1.0f / Lsum);
                     }
                     __syncthreads();
                     if (tid < 32) put_g(g_xo, (long)m * (D / 2) + h * 32 + tid, tag(l, 5), pack2<T>(res[2 * tid], res[2 * tid + 1]));
+                    __syncthreads();  // part (in xs) read before phase F's sweep writes xs
                 }
                 stamp(l, 4, 1);
             }
         }
         // ---- F: cross-out projection + residual -------------------------------------------------------------------
         {
+            wf1.load(W.f1, 4 * D, D, true);
             if (!sweep_xs(g_xo, D / 2, tag(l, 5))) return;
             stamp(l, 5, 0);
             float acc[NC1][MAXM];
@@ -754,7 +736,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             wf2.load(W.f2, D, 4 * D, false);
             if (!sweep_xf(g_x2, tag(l, 6))) return;
             stamp(l, 6, 0);
-            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs);
+            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs, lred);
             __syncthreads();
             float acc[NC4][MAXM];
             wf1.template run<MAXM>(xs, D, M, acc);
@@ -795,7 +777,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
     if (w0 == 0) {
         if (!sweep_xf(g_x0, tag(L, 0))) return;
-        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh);
+        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh, lred);
     }
 }
 
