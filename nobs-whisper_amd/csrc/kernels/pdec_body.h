@@ -85,11 +85,6 @@ __device__ __forceinline__ float wave_max(float x) {
     return x;
 }
 
-__device__ __forceinline__ float gelu_t(float x, const uint16_t* tab) {  // == gelu_ggml (gemm.hip gelu_tab)
-    if (x <= -10.0f) return 0.0f;
-    if (x >= 10.0f) return x;
-    return (float)__builtin_bit_cast(half_t, tab[__builtin_bit_cast(uint16_t, (half_t)x)]);
-}
 
 }  // namespace
 
@@ -130,15 +125,18 @@ template <typename T, int NCW, int NV, bool Q>
 struct ColSlice {
     static constexpr int NB = NV / 3;
     u32x4 w[NCW][NV];
+    float bias[NCW];  // the bias of each of the lane's columns (loaded with the weights: no dependent load later)
     int c0, nc, K, qt;
     // pairs: slices of whole column pairs (2i, 2i + 1), for outputs handed off as packed T pairs
-    __device__ __forceinline__ void load(const PdecMat& W, int N, int K_, bool pairs) {
+    __device__ __forceinline__ void load(const PdecMat& W, const float* b, int N, int K_, bool pairs) {
         K = K_;
         qt = Q ? W.qt : 0;
         const int w0 = blockIdx.x, u = pairs ? 2 : 1, nu = N / u;
         c0 = u * (int)((long)w0 * nu / kG);
         nc = u * (int)((long)(w0 + 1) * nu / kG) - c0;
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < NCW; j++) bias[j] = wave + 4 * j < nc ? *gp(b + c0 + wave + 4 * j) : 0.0f;
         if (!Q) {
             const int nvec = K >> 3;
 #pragma unroll
@@ -248,26 +246,31 @@ struct ColSlice {
 // LayerNorm of rows [0, M) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
 // layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over wpr = 4 / M
 // waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
-// per row. The row is re-read from LDS in each pass (no register copy: the weights of the next phases
-// are held in registers meanwhile).
+// per row; lane l of a row's wave q holds elements k = l + 64 (q + wpr e). The row is re-read from LDS in
+// each pass. (gamma / beta are global loads: the phases issue no weight stream ahead of a LayerNorm
+// that these loads would wait behind, except phase D's small cross-out slice.)
 template <typename T, int D>
-__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __restrict__ w, const float* __restrict__ b, T* out,
-                                        double* lred) {
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw, const float* gb, T* out, double* lred) {
 #pragma clang fp contract(off)
+    constexpr int NPL = (D + 63) / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wpr = M == 1 ? 4 : (M == 2 ? 2 : 1);  // uniform
     const int nrow = M < 3 ? M : 4;                  // rows handled at once
+    const int q = wave % wpr;
     auto wsum = [](double x) {
         for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
         return x;
     };
     for (int m0 = 0; m0 < M; m0 += nrow) {
-        const int m = m0 + wave / wpr, q = wave % wpr;
+        const int m = m0 + wave / wpr;
         const bool on = m < M;
         const float* x = xf + (long)m * D;
         double s = 0.0;
-        if (on)
-            for (int k = lane + 64 * q; k < D; k += 64 * wpr) s += (double)x[k];
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * (q + wpr * e);
+            if (on && k < D) s += (double)x[k];
+        }
         s = wsum(s);
         if (lane == 0) lred[wave] = s;
         __syncthreads();
@@ -275,11 +278,14 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __r
         for (int i = 0; i < wpr; i++) st += lred[(wave / wpr) * wpr + i];
         const float mean = (float)(st / D);
         double s2 = 0.0;
-        if (on)
-            for (int k = lane + 64 * q; k < D; k += 64 * wpr) {
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * (q + wpr * e);
+            if (on && k < D) {
                 const float v = x[k] - mean;
                 s2 += (double)(v * v);
             }
+        }
         s2 = wsum(s2);
         if (lane == 0) lred[4 + wave] = s2;
         __syncthreads();
@@ -287,12 +293,15 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* __r
         for (int i = 0; i < wpr; i++) st2 += lred[4 + (wave / wpr) * wpr + i];
         const float variance = (float)(st2 / D);
         const float scale = 1.0f / sqrtf(variance + 1e-5f);
-        if (on)
-            for (int k = lane + 64 * q; k < D; k += 64 * wpr) {
+#pragma unroll
+        for (int e = 0; e < NPL; e++) {
+            const int k = lane + 64 * (q + wpr * e);
+            if (on && k < D) {
                 float t = (x[k] - mean) * scale;
-                t = t * w[k];
-                out[(long)m * D + k] = (T)(t + b[k]);
+                t = t * *gp(gw + k);
+                out[(long)m * D + k] = (T)(t + *gp(gb + k));
             }
+        }
         __syncthreads();  // lred is rewritten by the next rows / call
     }
 }
@@ -545,7 +554,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     ColSlice<T, NCX, NV1, Q> wxq;
     ColSlice<T, NC4, NV1, Q> wf1;
     ColSlice<T, NC1, NV4, Q> wf2;
-    wq.load(a.layers[0].qkv, 3 * D, D, true);
+    wq.load(a.layers[0].qkv, a.layers[0].bqkv, 3 * D, D, true);
 
     for (int l = 0; l < L; l++) {
         const PdecLayer& W = a.layers[l];
@@ -580,7 +589,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     const int cl = wave + 4 * j;
                     if (m < M && cl < wq.nc && lane == m) {
                         const int n = wq.c0 + cl;
-                        float v = acc[j][m] + W.bqkv[n];
+                        float v = acc[j][m] + wq.bias[j];
                         if (n < 2 * D) v = v * a.k_scale;
                         ost[m * CMAX + cl] = (float)(T)v;
                     }
@@ -590,7 +599,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- B: self attention of (row, head) over the cache + this position (one task each) ----------------
         {
-            wo.load(W.o, D, D, false);
+            wo.load(W.o, W.bo, D, D, false);
             if (w0 < M * H) {
                 const int m = w0 / H, h = w0 % H;
                 const int pos = a.pos[m], nkv = pos + 1;
@@ -621,7 +630,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- C: out projection + residual -----------------------------------------------------------------------
         {
-            wxq.load(W.xq, D, D, true);
+            wxq.load(W.xq, W.bxq, D, D, true);
             if (!sweep_xs(g_so, D / 2, tag(l, 2))) return;
             stamp(l, 2, 0);
             float acc[NC1][MAXM];
@@ -633,7 +642,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     const int cl = wave + 4 * j;
                     if (m < M && cl < wo.nc && lane == m) {
                         const int n = wo.c0 + cl;
-                        xcur[j][m] = (acc[j][m] + W.bo[n]) + xcur[j][m];
+                        xcur[j][m] = (acc[j][m] + wo.bias[j]) + xcur[j][m];
                         put_g(g_x1, (long)m * D + n, tag(l, 3), __builtin_bit_cast(uint32_t, xcur[j][m]));
                     }
                 }
@@ -641,10 +650,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- D: LN + cross-Q projection (scaled; rounded to T) --------------------------------------------------
         {
-            wxo.load(W.xo, D, D, false);
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
             ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs, lred);
+            wxo.load(W.xo, W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
             __syncthreads();
             float acc[NCX][MAXM];
             wxq.template run<MAXM>(xs, D, M, acc);
@@ -655,7 +664,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     const int cl = wave + 4 * j;
                     if (m < M && cl < wxq.nc && lane == m) {
                         const int n = wxq.c0 + cl;
-                        ost[m * CMAX + cl] = (float)(T)((acc[j][m] + W.bxq[n]) * a.k_scale);
+                        ost[m * CMAX + cl] = (float)(T)((acc[j][m] + wxq.bias[j]) * a.k_scale);
                     }
                 }
             publish_pairs(g_qx, D / 2, wxq.c0, wxq.nc, tag(l, 4));
@@ -713,9 +722,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- F: cross-out projection + residual -------------------------------------------------------------------
         {
-            wf1.load(W.f1, 4 * D, D, true);
             if (!sweep_xs(g_xo, D / 2, tag(l, 5))) return;
             stamp(l, 5, 0);
+            wf1.load(W.f1, W.b1, 4 * D, D, true);  // streams under this phase's GEMV and phase G's wait
             float acc[NC1][MAXM];
             wxo.template run<MAXM>(xs, D, M, acc);
 #pragma unroll
@@ -725,7 +734,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     const int cl = wave + 4 * j;
                     if (m < M && cl < wxo.nc && lane == m) {
                         const int n = wxo.c0 + cl;
-                        xcur[j][m] = (acc[j][m] + W.bxo[n]) + xcur[j][m];
+                        xcur[j][m] = (acc[j][m] + wxo.bias[j]) + xcur[j][m];
                         put_g(g_x2, (long)m * D + n, tag(l, 6), __builtin_bit_cast(uint32_t, xcur[j][m]));
                     }
                 }
@@ -733,29 +742,43 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- G: LN + FC1 + GELU (ggml's f16 table; rounded to T) ----------------------------------------------
         {
-            wf2.load(W.f2, D, 4 * D, false);
             if (!sweep_xf(g_x2, tag(l, 6))) return;
             stamp(l, 6, 0);
             ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs, lred);
             __syncthreads();
             float acc[NC4][MAXM];
             wf1.template run<MAXM>(xs, D, M, acc);
+            // GELU by ggml's f16 table: the lookups are issued, then phase H's weights, then the lookups
+            // are used (waiting for them does not wait for the weight stream issued after them)
+            float gx[NC4];
+            uint16_t gt[NC4];
 #pragma unroll
-            for (int j = 0; j < NC4; j++)
+            for (int j = 0; j < NC4; j++) {
+                const int cl = wave + 4 * j;
+                gx[j] = 0.0f;
 #pragma unroll
-                for (int m = 0; m < MAXM; m++) {
-                    const int cl = wave + 4 * j;
-                    if (m < M && cl < wf1.nc && lane == m) {
-                        const int n = wf1.c0 + cl;
-                        ost[m * CMAX + cl] = (float)(T)gelu_t(acc[j][m] + W.b1[n], a.gelu_tab);
-                    }
+                for (int m = 0; m < MAXM; m++)
+                    if (lane == m) gx[j] = acc[j][m] + wf1.bias[j];
+                gt[j] = (lane < M && cl < wf1.nc) ? *gp(a.gelu_tab + __builtin_bit_cast(uint16_t, (half_t)gx[j])) : 0;
+            }
+            asm volatile("" ::: "memory");
+            wf2.load(W.f2, W.b2, D, 4 * D, false);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < NC4; j++) {
+                const int cl = wave + 4 * j;
+                if (lane < M && cl < wf1.nc) {
+                    const float x = gx[j];
+                    const float g = x <= -10.0f ? 0.0f : (x >= 10.0f ? x : (float)__builtin_bit_cast(half_t, gt[j]));
+                    ost[lane * CMAX + cl] = (float)(T)g;
                 }
+            }
             publish_pairs(g_ff, 2 * D, wf1.c0, wf1.nc, tag(l, 7));
             stamp(l, 6, 1);
         }
         // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
         {
-            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, 3 * D, D, true);
+            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);
             if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
             stamp(l, 7, 0);
             float acc[NC1][MAXM];
@@ -767,7 +790,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     const int cl = wave + 4 * j;
                     if (m < M && cl < wf2.nc && lane == m) {
                         const int n = wf2.c0 + cl;
-                        xcur[j][m] = (acc[j][m] + W.b2[n]) + xcur[j][m];
+                        xcur[j][m] = (acc[j][m] + wf2.bias[j]) + xcur[j][m];
                         put_g(g_x0, (long)m * D + n, tag(l + 1, 0), __builtin_bit_cast(uint32_t, xcur[j][m]));
                     }
                 }
