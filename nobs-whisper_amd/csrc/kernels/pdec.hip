@@ -46,14 +46,14 @@ int pdec_cross_splits(int M, int H, int rows) { return std::max(1, std::min(kG /
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
     if (a.M < 1 || a.M > kPdecMaxRows) WM_FAIL("pdec: %d rows", a.M);
     if (a.M * (a.d / 64) * a.s_cross > kG) WM_FAIL("pdec: split count");
-    // one attention chunk (16 rows per lane group) per task; the cross partials of a (clip, head) fit the
-    // LDS rows buffer of the merging workgroup
-    if (a.n_text_ctx > 16 * kNT / 8 || (a.n_audio_ctx + a.s_cross - 1) / a.s_cross > 16 * kNT / 8 ||
+    // self attention in one chunk (16 rows per lane group); cross-attention tasks of at most 1536 rows (the
+    // scores buffer); the cross partials of a (clip, head) fit the LDS rows buffer of the merging workgroup
+    if (a.n_text_ctx > 16 * kNT / 8 || (a.n_audio_ctx + a.s_cross - 1) / a.s_cross > 1536 ||
         (size_t)a.s_cross * 66 * 4 > (size_t)kPdecMaxRows * 4 * a.d * 2)
         WM_FAIL("pdec: context sizes");
     const int CMAX = std::max(2 * ((3 * a.d / 2 + kG - 1) / kG), 2 * ((2 * a.d + kG - 1) / kG));
     const size_t lds = (size_t)kPdecMaxRows * 4 * a.d * 2 + (size_t)kPdecMaxRows * a.d * 4 +
-                       (1536 + 8 + 256 + 192 + 68 + kPdecMaxRows * CMAX + 16 + 4) * sizeof(float);
+                       (1536 + 8 + 256 + 192 + 68 + kPdecMaxRows * CMAX + 16 + 2 * (size_t)a.d + 4) * sizeof(float);
     WM_CHECK(hipMemsetAsync(a.sync, 0, a.gr.bytes, st));
     if (a.quant) {
         if (dt != DType::F16) WM_FAIL("pdec: GGML blocks with a bf16 context");

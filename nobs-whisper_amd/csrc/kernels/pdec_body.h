@@ -243,67 +243,75 @@ struct ColSlice {
     }
 };
 
-// LayerNorm of rows [0, M) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
+// LayerNorm of rows [0, M <= 4) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
 // layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over wpr = 4 / M
 // waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
-// per row; lane l of a row's wave q holds elements k = l + 64 (q + wpr e). The row is re-read from LDS in
-// each pass. (gamma / beta are global loads: the phases issue no weight stream ahead of a LayerNorm
-// that these loads would wait behind, except phase D's small cross-out slice.)
+// per row; lane l of a row's wave q holds elements k = l + 64 (q + wpr e), re-read from LDS in each pass.
+// gamma / beta: every thread loads its share first (2d / 256 values), stores it to lnp (LDS [2d]) after the
+// first pass, so the loads land under the sums and the last pass reads LDS.
 template <typename T, int D>
-__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw, const float* gb, T* out, double* lred) {
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw, const float* gb, T* out, double* lred,
+                                        float* lnp) {
 #pragma clang fp contract(off)
-    constexpr int NPL = (D + 63) / 64;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int NPL = (D + 63) / 64, NGB = (2 * D + kNT - 1) / kNT;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int wpr = M == 1 ? 4 : (M == 2 ? 2 : 1);  // uniform
-    const int nrow = M < 3 ? M : 4;                  // rows handled at once
-    const int q = wave % wpr;
-    auto wsum = [](double x) {
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-        return x;
+    const int q = wave % wpr, m = wave / wpr;
+    const bool on = m < M;
+    const float* x = xf + (long)m * D;
+    auto wsum = [](double v) {
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        return v;
     };
-    for (int m0 = 0; m0 < M; m0 += nrow) {
-        const int m = m0 + wave / wpr;
-        const bool on = m < M;
-        const float* x = xf + (long)m * D;
-        double s = 0.0;
+    float gb_[NGB];
 #pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * (q + wpr * e);
-            if (on && k < D) s += (double)x[k];
-        }
-        s = wsum(s);
-        if (lane == 0) lred[wave] = s;
-        __syncthreads();
-        double st = 0.0;
-        for (int i = 0; i < wpr; i++) st += lred[(wave / wpr) * wpr + i];
-        const float mean = (float)(st / D);
-        double s2 = 0.0;
-#pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * (q + wpr * e);
-            if (on && k < D) {
-                const float v = x[k] - mean;
-                s2 += (double)(v * v);
-            }
-        }
-        s2 = wsum(s2);
-        if (lane == 0) lred[4 + wave] = s2;
-        __syncthreads();
-        double st2 = 0.0;
-        for (int i = 0; i < wpr; i++) st2 += lred[4 + (wave / wpr) * wpr + i];
-        const float variance = (float)(st2 / D);
-        const float scale = 1.0f / sqrtf(variance + 1e-5f);
-#pragma unroll
-        for (int e = 0; e < NPL; e++) {
-            const int k = lane + 64 * (q + wpr * e);
-            if (on && k < D) {
-                float t = (x[k] - mean) * scale;
-                t = t * *gp(gw + k);
-                out[(long)m * D + k] = (T)(t + *gp(gb + k));
-            }
-        }
-        __syncthreads();  // lred is rewritten by the next rows / call
+    for (int u = 0; u < NGB; u++) {
+        const int i = tid + kNT * u;
+        gb_[u] = i < D ? *gp(gw + i) : (i < 2 * D ? *gp(gb + (i - D)) : 0.0f);
     }
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * (q + wpr * e);
+        if (on && k < D) s += (double)x[k];
+    }
+    s = wsum(s);
+    if (lane == 0) lred[wave] = s;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NGB; u++) {
+        const int i = tid + kNT * u;
+        if (i < 2 * D) lnp[i] = gb_[u];
+    }
+    double st = 0.0;
+    for (int i = 0; i < wpr; i++) st += lred[m * wpr + i];
+    const float mean = (float)(st / D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * (q + wpr * e);
+        if (on && k < D) {
+            const float v = x[k] - mean;
+            s2 += (double)(v * v);
+        }
+    }
+    s2 = wsum(s2);
+    if (lane == 0) lred[4 + wave] = s2;
+    __syncthreads();  // (also lnp complete)
+    double st2 = 0.0;
+    for (int i = 0; i < wpr; i++) st2 += lred[4 + m * wpr + i];
+    const float variance = (float)(st2 / D);
+    const float scale = 1.0f / sqrtf(variance + 1e-5f);
+#pragma unroll
+    for (int e = 0; e < NPL; e++) {
+        const int k = lane + 64 * (q + wpr * e);
+        if (on && k < D) {
+            float t = (x[k] - mean) * scale;
+            t = t * lnp[k];
+            out[(long)m * D + k] = (T)(t + lnp[D + k]);
+        }
+    }
+    __syncthreads();  // lred, lnp are rewritten by the next call
 }
 
 // ---- hand-offs: data-tagged granules ----------------------------------------------------------------------
@@ -378,56 +386,59 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
     return r;
 }
 
-// Attention over keys/values rows [r0, r1) of (K, V) [rows][64] T, at most 32 U rows (one chunk):
-// 32 lane groups of 8 lanes, a key row per group, U rows per group. attn_load issues every K and V row
-// load of the range into registers (rows from earlier launches: before the wait for this step's query);
-// row `fresh` (this position's k, v, handed off in this launch) is not loaded: attn_task takes it from
-// fk / fv (LDS f32). attn_task leaves in res (LDS): o[64] = sum_t p_t v_t, res[64] = max score,
-// res[65] = sum_t p_t, with p_t = e^(s_t - max) (rounded to T as the P.V operand).
+// Attention over keys/values rows [r0, r1) of (K, V) [rows][64] T (at most 1536 rows): 32 lane groups of
+// 8 lanes, a key row per group, chunks of 32 U rows. attn_load issues every K and V row load of the first
+// chunk into registers (rows from earlier launches: before the wait for this step's query); row `fresh`
+// (this position's k, v, handed off in this launch) is not loaded: attn_task takes it from fk / fv (LDS
+// f32). Later chunks (ranges over 32 U rows) are loaded by attn_task into the K registers once the first
+// chunk's keys are scored (MULTI; a task of one chunk compiles without the loops). Leaves in res (LDS): o[64] = sum_t p_t v_t, res[64] = max score, res[65] =
+// sum_t p_t, with p_t = e^(s_t - max) (rounded to T as the P.V operand).
 template <typename T, int U>
-__device__ __forceinline__ void attn_load(const T* __restrict__ K, const T* __restrict__ V, int r0, int r1, int fresh,
-                                          u32x4 (&rk)[U], u32x4 (&rv)[U]) {
+__device__ __forceinline__ void attn_rows(const T* __restrict__ X, int t0, int r1, int fresh, u32x4 (&r)[U]) {
     const int lane8 = threadIdx.x & 7, grp = threadIdx.x >> 3;
     constexpr int NG = kNT / 8;
     const u32x4 zero = {0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const int t = r0 + grp + NG * u;
-        const bool in = t < r1 && t != fresh;
-        rk[u] = in ? *gp((const u32x4*)(K + (long)t * 64 + lane8 * 8)) : zero;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const int t = r0 + grp + NG * u;
-        const bool in = t < r1 && t != fresh;
-        rv[u] = in ? *gp((const u32x4*)(V + (long)t * 64 + lane8 * 8)) : zero;
+        const int t = t0 + grp + NG * u;
+        r[u] = (t < r1 && t != fresh) ? *gp((const u32x4*)(X + (long)t * 64 + lane8 * 8)) : zero;
     }
 }
 template <typename T, int U>
-__device__ __forceinline__ void attn_task(const float* qs, const u32x4 (&rk)[U], const u32x4 (&rv)[U], int r0, int r1,
-                                          int fresh, const float* fk, const float* fv, float* sc, float* red, float* res) {
+__device__ __forceinline__ void attn_load(const T* __restrict__ K, const T* __restrict__ V, int r0, int r1, int fresh,
+                                          u32x4 (&rk)[U], u32x4 (&rv)[U]) {
+    attn_rows<T, U>(K, r0, r1, fresh, rk);
+    attn_rows<T, U>(V, r0, r1, fresh, rv);
+}
+template <typename T, int U, bool MULTI>
+__device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, u32x4 (&rk)[U],
+                                          const u32x4 (&rv)[U], int r0, int r1, int fresh, const float* fk, const float* fv,
+                                          float* sc, float* red, float* res) {
     const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
-    constexpr int NG = kNT / 8;
+    constexpr int NG = kNT / 8, CH = NG * U;
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
     float lmax = -INFINITY;
+    for (int c0 = r0; c0 < (MULTI ? r1 : r0 + 1); c0 += CH) {
+        if (c0 != r0) attn_rows<T, U>(K, c0, r1, fresh, rk);
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        const int t = r0 + grp + NG * u;
-        const T* ke = (const T*)&rk[u];
-        float a = 0.0f;
-        if (t == fresh) {
+        for (int u = 0; u < U; u++) {
+            const int t = c0 + grp + NG * u;
+            const T* ke = (const T*)&rk[u];
+            float a = 0.0f;
+            if (t == fresh) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
-        } else {
+                for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
+            } else {
 #pragma unroll
-            for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-        }
-        a = sum8(a);
-        if (t < r1) {
-            if (lane8 == 0) sc[t - r0] = a;
-            lmax = fmaxf(lmax, a);
+                for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
+            }
+            a = sum8(a);
+            if (t < r1) {
+                if (lane8 == 0) sc[t - r0] = a;
+                lmax = fmaxf(lmax, a);
+            }
         }
     }
     lmax = wave_max(lmax);
@@ -446,20 +457,27 @@ __device__ __forceinline__ void attn_task(const float* qs, const u32x4 (&rk)[U],
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
+    auto pv = [&](int c0, const u32x4 (&r)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        const int t = r0 + grp + NG * u;
-        if (t < r1) {
-            const float p = sc[t - r0];
-            if (t == fresh) {
+        for (int u = 0; u < U; u++) {
+            const int t = c0 + grp + NG * u;
+            if (t < r1) {
+                const float p = sc[t - r0];
+                if (t == fresh) {
 #pragma unroll
-                for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
-            } else {
-                const T* ve = (const T*)&rv[u];
+                    for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
+                } else {
+                    const T* ve = (const T*)&r[u];
 #pragma unroll
-                for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+                    for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
+                }
             }
         }
+    };
+    pv(r0, rv);
+    for (int c0 = r0 + CH; MULTI && c0 < r1; c0 += CH) {
+        attn_rows<T, U>(V, c0, r1, fresh, rk);
+        pv(c0, rk);
     }
     // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by shuffles, then over the 4 waves in LDS
 #pragma unroll
@@ -505,7 +523,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     float* res = qf + 192;                                            // attention result [64 + 2] (+ pad)
     float* ost = res + 68;                                            // packed outputs [M][CMAX]
     double* lred = (double*)(ost + MAXM * CMAX);                      // LayerNorm partial sums [8]
-    int* lflag = (int*)(lred + 8);
+    float* lnp = (float*)(lred + 8);                                  // LayerNorm gamma, beta [2d]
+    int* lflag = (int*)(lnp + 2 * D);
 
     const int M = a.M, L = a.L, w0 = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const PdecGranules& G = a.gr;
@@ -578,7 +597,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 return;
             }
             stamp(l, 0, 0);
-            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs, lred);
+            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs, lred, lnp);
             __syncthreads();
             float acc[NCQ][MAXM];
             wq.template run<MAXM>(xs, D, M, acc);
@@ -620,7 +639,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     Kc[(long)pos * 64 + tid] = (T)qf[64 + tid];
                     Vc[(long)pos * 64 + tid] = (T)qf[128 + tid];
                 }
-                attn_task<T, 16>(qf, rk, rv, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
+                attn_task<T, 16, false>(qf, Kc, Vc, rk, rv, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
                 if (tid < 32) {
                     const float inv = 1.0f / res[65];
                     put_g(g_so, (long)m * (D / 2) + h * 32 + tid, tag(l, 2), pack2<T>(res[2 * tid] * inv, res[2 * tid + 1] * inv));
@@ -652,7 +671,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
-            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs, lred);
+            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs, lred, lnp);
             wxo.load(W.xo, W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
             __syncthreads();
             float acc[NCX][MAXM];
@@ -680,8 +699,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 const long sl = a.slot[m];
                 const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
                 const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
-                u32x4 rk[16], rv[16];
-                attn_load<T, 16>(Kc, Vc, r0, r1, -1, rk, rv);  // constant for the window: issued before the wait
+                u32x4 rk[8], rv[8];
+                attn_load<T, 8>(Kc, Vc, r0, r1, -1, rk, rv);  // constant for the window: issued before the wait
                 if (!sweep(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
                            [&](int i, uint32_t b) {
                                qf[2 * i] = (float)lo_t<T>(b);
@@ -689,7 +708,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 4, 0);
-                attn_task<T, 16>(qf, rk, rv, r0, r1, -1, nullptr, nullptr, sc, red, res);
+                attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, nullptr, nullptr, sc, red, res);
                 // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
                 // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
                 unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
@@ -744,7 +763,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             if (!sweep_xf(g_x2, tag(l, 6))) return;
             stamp(l, 6, 0);
-            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs, lred);
+            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs, lred, lnp);
             __syncthreads();
             float acc[NC4][MAXM];
             wf1.template run<MAXM>(xs, D, M, acc);
@@ -778,9 +797,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
         {
-            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);
             if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
             stamp(l, 7, 0);
+            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);  // under the GEMV
             float acc[NC1][MAXM];
             wf2.template run<MAXM>(xs, 4 * D, M, acc);
 #pragma unroll
@@ -800,7 +819,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
     if (w0 == 0) {
         if (!sweep_xf(g_x0, tag(L, 0))) return;
-        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh, lred);
+        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh, lred, lnp);
     }
 }
 
