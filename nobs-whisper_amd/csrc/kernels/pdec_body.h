@@ -76,13 +76,60 @@ __device__ __forceinline__ float sum8(float a) {
     a += dppf<0x4E>(a);
     return a + dppf<0x141>(a);
 }
+// Whole-wave reductions without LDS round trips: DPP inside a 16-lane row (xor 1, xor 2, half-row mirror,
+// row mirror), then the gfx950 permlane swaps across rows (xor 16, xor 32). Every step pairs two values
+// symmetrically, so every lane ends with the same bits.
+__device__ __forceinline__ float xor16_other(float x, float& y) {  // y: the value of lane ^ 16
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x), false, false);
+    y = __builtin_bit_cast(float, r[1]);
+    return __builtin_bit_cast(float, r[0]);
+}
+__device__ __forceinline__ float xor32_other(float x, float& y) {  // y: the value of lane ^ 32
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x), false, false);
+    y = __builtin_bit_cast(float, r[1]);
+    return __builtin_bit_cast(float, r[0]);
+}
+__device__ __forceinline__ float sum_x16(float x) { float y; const float z = xor16_other(x, y); return z + y; }
+__device__ __forceinline__ float sum_x32(float x) { float y; const float z = xor32_other(x, y); return z + y; }
 __device__ __forceinline__ float wave_sum(float x) {
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
+    x += dppf<0xB1>(x);
+    x += dppf<0x4E>(x);
+    x += dppf<0x141>(x);
+    x += dppf<0x140>(x);
+    return sum_x32(sum_x16(x));
 }
 __device__ __forceinline__ float wave_max(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-    return x;
+    x = fmaxf(x, dppf<0xB1>(x));
+    x = fmaxf(x, dppf<0x4E>(x));
+    x = fmaxf(x, dppf<0x141>(x));
+    x = fmaxf(x, dppf<0x140>(x));
+    float y;
+    float z = xor16_other(x, y);
+    x = fmaxf(z, y);
+    z = xor32_other(x, y);
+    return fmaxf(z, y);
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double x) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)b, CTRL, 0xF, 0xF, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int W>  // 16 or 32
+__device__ __forceinline__ double sum_xw(double x) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    const auto l = W == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false) : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = W == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false) : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __builtin_bit_cast(double, ((uint64_t)h[0] << 32) | l[0]) + __builtin_bit_cast(double, ((uint64_t)h[1] << 32) | l[1]);
+}
+__device__ __forceinline__ double wave_sum_d(double x) {
+    x += dppd<0xB1>(x);
+    x += dppd<0x4E>(x);
+    x += dppd<0x141>(x);
+    x += dppd<0x140>(x);
+    return sum_xw<32>(sum_xw<16>(x));
 }
 
 
@@ -238,8 +285,7 @@ struct ColSlice {
 #pragma unroll
         for (int j = 0; j < NCW; j++)
 #pragma unroll
-            for (int m = 0; m < MAXM; m++)
-                if (m < M && wave + 4 * j < nc) acc[j][m] = wave_sum(acc[j][m]);
+            for (int m = 0; m < MAXM; m++) acc[j][m] = wave_sum(acc[j][m]);  // (branch-free: the chains interleave)
     }
 };
 
@@ -259,10 +305,6 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
     const int q = wave % wpr, m = wave / wpr;
     const bool on = m < M;
     const float* x = xf + (long)m * D;
-    auto wsum = [](double v) {
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        return v;
-    };
     float gb_[NGB];
 #pragma unroll
     for (int u = 0; u < NGB; u++) {
@@ -275,7 +317,7 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
         const int k = lane + 64 * (q + wpr * e);
         if (on && k < D) s += (double)x[k];
     }
-    s = wsum(s);
+    s = wave_sum_d(s);
     if (lane == 0) lred[wave] = s;
     __syncthreads();
 #pragma unroll
@@ -295,7 +337,7 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
             s2 += (double)(v * v);
         }
     }
-    s2 = wsum(s2);
+    s2 = wave_sum_d(s2);
     if (lane == 0) lred[4 + wave] = s2;
     __syncthreads();  // (also lnp complete)
     double st2 = 0.0;
@@ -479,13 +521,9 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
         attn_rows<T, U>(V, c0, r1, fresh, rk);
         pv(c0, rk);
     }
-    // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by shuffles, then over the 4 waves in LDS
+    // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by DPP / permlane swaps, then over the 4 waves in LDS
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-        acc[e] += __shfl_xor(acc[e], 8);
-        acc[e] += __shfl_xor(acc[e], 16);
-        acc[e] += __shfl_xor(acc[e], 32);
-    }
+    for (int e = 0; e < 8; e++) acc[e] = sum_x32(sum_x16(acc[e] + dppf<0x128>(acc[e])));  // xor 8 (row rotate 8), 16, 32
     __syncthreads();
     float* ow = red + 8;  // [4 waves][64]
     if (lane < 8) {
