@@ -76,38 +76,26 @@ __device__ __forceinline__ float sum8(float a) {
     a += dppf<0x4E>(a);
     return a + dppf<0x141>(a);
 }
-// Whole-wave reductions without LDS round trips: DPP inside a 16-lane row (xor 1, xor 2, half-row mirror,
-// row mirror), then the gfx950 permlane swaps across rows (xor 16, xor 32). Every step pairs two values
-// symmetrically, so every lane ends with the same bits.
-__device__ __forceinline__ float xor16_other(float x, float& y) {  // y: the value of lane ^ 16
-    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x), false, false);
-    y = __builtin_bit_cast(float, r[1]);
-    return __builtin_bit_cast(float, r[0]);
+// Whole-wave reductions without LDS round trips: DPP inside each 16-lane row (xor 1, xor 2, half-row
+// mirror, row mirror: every lane ends with its row's sum), then the four row sums read as scalars and
+// added in row order, so every lane gets the same bits. (tools/probe/wave_reduce.hip checks the DPP
+// lane maps on the device.)
+__device__ __forceinline__ float lane_f(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
-__device__ __forceinline__ float xor32_other(float x, float& y) {  // y: the value of lane ^ 32
-    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x), false, false);
-    y = __builtin_bit_cast(float, r[1]);
-    return __builtin_bit_cast(float, r[0]);
-}
-__device__ __forceinline__ float sum_x16(float x) { float y; const float z = xor16_other(x, y); return z + y; }
-__device__ __forceinline__ float sum_x32(float x) { float y; const float z = xor32_other(x, y); return z + y; }
 __device__ __forceinline__ float wave_sum(float x) {
     x += dppf<0xB1>(x);
     x += dppf<0x4E>(x);
     x += dppf<0x141>(x);
     x += dppf<0x140>(x);
-    return sum_x32(sum_x16(x));
+    return (lane_f(x, 0) + lane_f(x, 16)) + (lane_f(x, 32) + lane_f(x, 48));
 }
 __device__ __forceinline__ float wave_max(float x) {
     x = fmaxf(x, dppf<0xB1>(x));
     x = fmaxf(x, dppf<0x4E>(x));
     x = fmaxf(x, dppf<0x141>(x));
     x = fmaxf(x, dppf<0x140>(x));
-    float y;
-    float z = xor16_other(x, y);
-    x = fmaxf(z, y);
-    z = xor32_other(x, y);
-    return fmaxf(z, y);
+    return fmaxf(fmaxf(lane_f(x, 0), lane_f(x, 16)), fmaxf(lane_f(x, 32), lane_f(x, 48)));
 }
 template <int CTRL>
 __device__ __forceinline__ double dppd(double x) {
@@ -116,20 +104,17 @@ __device__ __forceinline__ double dppd(double x) {
     const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-template <int W>  // 16 or 32
-__device__ __forceinline__ double sum_xw(double x) {
+__device__ __forceinline__ double lane_d(double x, int l) {
     const uint64_t b = __builtin_bit_cast(uint64_t, x);
-    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
-    const auto l = W == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false) : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto h = W == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false) : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    return __builtin_bit_cast(double, ((uint64_t)h[0] << 32) | l[0]) + __builtin_bit_cast(double, ((uint64_t)h[1] << 32) | l[1]);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ double wave_sum_d(double x) {
     x += dppd<0xB1>(x);
     x += dppd<0x4E>(x);
     x += dppd<0x141>(x);
     x += dppd<0x140>(x);
-    return sum_xw<32>(sum_xw<16>(x));
+    return (lane_d(x, 0) + lane_d(x, 16)) + (lane_d(x, 32) + lane_d(x, 48));
 }
 
 
@@ -521,9 +506,13 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
         attn_rows<T, U>(V, c0, r1, fresh, rk);
         pv(c0, rk);
     }
-    // reduce over the 8 groups of a wave (lanes lane8 + 8 g) by DPP / permlane swaps, then over the 4 waves in LDS
+    // reduce over the 8 groups of a wave (lanes lane8 + 8 g): DPP for xor 8, permutes for 16 and 32; then over the 4 waves in LDS
 #pragma unroll
-    for (int e = 0; e < 8; e++) acc[e] = sum_x32(sum_x16(acc[e] + dppf<0x128>(acc[e])));  // xor 8 (row rotate 8), 16, 32
+    for (int e = 0; e < 8; e++) acc[e] += dppf<0x128>(acc[e]);  // xor 8 (row rotate by 8)
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] += __shfl_xor(acc[e], 16);  // (8 independent permutes per round)
+#pragma unroll
+    for (int e = 0; e < 8; e++) acc[e] += __shfl_xor(acc[e], 32);
     __syncthreads();
     float* ow = red + 8;  // [4 waves][64]
     if (lane < 8) {
