@@ -53,7 +53,7 @@ void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
         WM_FAIL("pdec: context sizes");
     const int CMAX = std::max(2 * ((3 * a.d / 2 + kG - 1) / kG), 2 * ((2 * a.d + kG - 1) / kG));
     const size_t lds = (size_t)kPdecMaxRows * 4 * a.d * 2 + (size_t)kPdecMaxRows * a.d * 4 +
-                       (1536 + 8 + 256 + 192 + 68 + kPdecMaxRows * CMAX + 16 + 2 * (size_t)a.d + 4) * sizeof(float);
+                       (1536 + 8 + 256 + 192 + 68 + kPdecMaxRows * CMAX + 16 + 6 * (size_t)a.d + 4) * sizeof(float);
     WM_CHECK(hipMemsetAsync(a.sync, 0, a.gr.bytes, st));
     if (a.quant) {
         if (dt != DType::F16) WM_FAIL("pdec: GGML blocks with a bf16 context");

@@ -66,6 +66,14 @@ __device__ __forceinline__ const __attribute__((address_space(1))) P* gp(const P
     return (const __attribute__((address_space(1))) P*)p;
 }
 
+// The thread index as a value the compiler cannot treat as loop-invariant: per-lane addresses are then
+// recomputed where they are used instead of being hoisted out of the layer loop and held in registers
+// for the whole kernel (which cost ~250 registers of this one-wave-per-SIMD kernel)
+__device__ __forceinline__ int ptid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
@@ -166,7 +174,7 @@ struct ColSlice {
         const int w0 = blockIdx.x, u = pairs ? 2 : 1, nu = N / u;
         c0 = u * (int)((long)w0 * nu / kG);
         nc = u * (int)((long)(w0 + 1) * nu / kG) - c0;
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int wave = ptid() >> 6, lane = ptid() & 63;
 #pragma unroll
         for (int j = 0; j < NCW; j++) bias[j] = wave + 4 * j < nc ? *gp(b + c0 + wave + 4 * j) : 0.0f;
         if (!Q) {
@@ -214,7 +222,7 @@ struct ColSlice {
     // acc[j][m] (all lanes) = sum_k xs[m][k] * W[c0 + wave + 4j][k]
     template <int MAXM>
     __device__ __forceinline__ void run(const T* xs, int ldx, int M, float (&acc)[NCW][MAXM]) const {
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int wave = ptid() >> 6, lane = ptid() & 63;
 #pragma unroll
         for (int j = 0; j < NCW; j++)
 #pragma unroll
@@ -278,24 +286,16 @@ struct ColSlice {
 // layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over wpr = 4 / M
 // waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
 // per row; lane l of a row's wave q holds elements k = l + 64 (q + wpr e), re-read from LDS in each pass.
-// gamma / beta: every thread loads its share first (2d / 256 values), stores it to lnp (LDS [2d]) after the
-// first pass, so the loads land under the sums and the last pass reads LDS.
+// gamma / beta (gam, bet) are LDS copies staged by phase A (stage_ln in the kernel), off the critical path.
 template <typename T, int D>
-__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw, const float* gb, T* out, double* lred,
-                                        float* lnp) {
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gam, const float* bet, T* out, double* lred) {
 #pragma clang fp contract(off)
-    constexpr int NPL = (D + 63) / 64, NGB = (2 * D + kNT - 1) / kNT;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr int NPL = (D + 63) / 64;
+    const int tid = ptid(), wave = tid >> 6, lane = tid & 63;
     const int wpr = M == 1 ? 4 : (M == 2 ? 2 : 1);  // uniform
     const int q = wave % wpr, m = wave / wpr;
     const bool on = m < M;
     const float* x = xf + (long)m * D;
-    float gb_[NGB];
-#pragma unroll
-    for (int u = 0; u < NGB; u++) {
-        const int i = tid + kNT * u;
-        gb_[u] = i < D ? *gp(gw + i) : (i < 2 * D ? *gp(gb + (i - D)) : 0.0f);
-    }
     double s = 0.0;
 #pragma unroll
     for (int e = 0; e < NPL; e++) {
@@ -305,11 +305,6 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
     s = wave_sum_d(s);
     if (lane == 0) lred[wave] = s;
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < NGB; u++) {
-        const int i = tid + kNT * u;
-        if (i < 2 * D) lnp[i] = gb_[u];
-    }
     double st = 0.0;
     for (int i = 0; i < wpr; i++) st += lred[m * wpr + i];
     const float mean = (float)(st / D);
@@ -324,7 +319,7 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
     }
     s2 = wave_sum_d(s2);
     if (lane == 0) lred[4 + wave] = s2;
-    __syncthreads();  // (also lnp complete)
+    __syncthreads();
     double st2 = 0.0;
     for (int i = 0; i < wpr; i++) st2 += lred[4 + m * wpr + i];
     const float variance = (float)(st2 / D);
@@ -334,11 +329,11 @@ __device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gw,
         const int k = lane + 64 * (q + wpr * e);
         if (on && k < D) {
             float t = (x[k] - mean) * scale;
-            t = t * lnp[k];
-            out[(long)m * D + k] = (T)(t + lnp[D + k]);
+            t = t * gam[k];
+            out[(long)m * D + k] = (T)(t + bet[k]);
         }
     }
-    __syncthreads();  // lred, lnp are rewritten by the next call
+    __syncthreads();  // lred is rewritten by the next call
 }
 
 // ---- hand-offs: data-tagged granules ----------------------------------------------------------------------
@@ -380,7 +375,7 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
             bool done = true;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int i = b + threadIdx.x + kNT * u;
+                const int i = b + ptid() + kNT * u;
                 v[u] = i < n ? get_g(g, addr(i)) : (unsigned long long)tag << 32;
                 done &= (unsigned)(v[u] >> 32) == tag;
             }
@@ -401,7 +396,7 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
         if (ok) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int i = b + threadIdx.x + kNT * u;
+                const int i = b + ptid() + kNT * u;
                 if (i < n) put(i, (uint32_t)v[u]);
             }
         }
@@ -422,7 +417,7 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
 // sum_t p_t, with p_t = e^(s_t - max) (rounded to T as the P.V operand).
 template <typename T, int U>
 __device__ __forceinline__ void attn_rows(const T* __restrict__ X, int t0, int r1, int fresh, u32x4 (&r)[U]) {
-    const int lane8 = threadIdx.x & 7, grp = threadIdx.x >> 3;
+    const int lane8 = ptid() & 7, grp = ptid() >> 3;
     constexpr int NG = kNT / 8;
     const u32x4 zero = {0, 0, 0, 0};
 #pragma unroll
@@ -441,7 +436,7 @@ template <typename T, int U, bool MULTI>
 __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, u32x4 (&rk)[U],
                                           const u32x4 (&rv)[U], int r0, int r1, int fresh, const float* fk, const float* fv,
                                           float* sc, float* red, float* res) {
-    const int tid = threadIdx.x, lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
+    const int tid = ptid(), lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
     constexpr int NG = kNT / 8, CH = NG * U;
     float qv[8];
 #pragma unroll
@@ -550,10 +545,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     float* res = qf + 192;                                            // attention result [64 + 2] (+ pad)
     float* ost = res + 68;                                            // packed outputs [M][CMAX]
     double* lred = (double*)(ost + MAXM * CMAX);                      // LayerNorm partial sums [8]
-    float* lnp = (float*)(lred + 8);                                  // LayerNorm gamma, beta [2d]
-    int* lflag = (int*)(lnp + 2 * D);
+    float* lnp = (float*)(lred + 8);                                  // LayerNorm gamma, beta [6][d]
+    int* lflag = (int*)(lnp + 6 * D);
 
-    const int M = a.M, L = a.L, w0 = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int M = a.M, L = a.L, w0 = blockIdx.x, tid = ptid(), wave = tid >> 6, lane = tid & 63;
     const PdecGranules& G = a.gr;
     unsigned long long* gb = (unsigned long long*)a.sync;
     unsigned long long *g_x0 = gb + G.x0, *g_x1 = gb + G.x1, *g_x2 = gb + G.x2, *g_qkv = gb + G.qkv;
@@ -602,6 +597,28 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     ColSlice<T, NC1, NV4, Q> wf2;
     wq.load(a.layers[0].qkv, a.layers[0].bqkv, 3 * D, D, true);
 
+    // LayerNorm gamma / beta into lnp slots (LN1 at 0, 1; cross LN at 2, 3; LN2 at 4, 5): issued into
+    // registers before the wait of the phase ahead of the LayerNorm's phase (C for the cross LN, F for LN2,
+    // H for the next layer's LN1 or the final LN), so they land under that wait, and stored after it
+    constexpr int NGL = (2 * D + kNT - 1) / kNT;
+    float lv[NGL];
+    auto ln_issue = [&](const float* gw, const float* gb) {
+#pragma unroll
+        for (int u = 0; u < NGL; u++) {
+            const int i = tid + kNT * u;
+            lv[u] = i < D ? *gp(gw + i) : (i < 2 * D ? *gp(gb + (i - D)) : 0.0f);
+        }
+    };
+    auto ln_commit = [&](int slot) {
+#pragma unroll
+        for (int u = 0; u < NGL; u++) {
+            const int i = tid + kNT * u;
+            if (i < 2 * D) lnp[slot * D + i] = lv[u];
+        }
+    };
+    ln_issue(a.layers[0].ln1_w, a.layers[0].ln1_b);
+    ln_commit(0);
+
     for (int l = 0; l < L; l++) {
         const PdecLayer& W = a.layers[l];
         // ---- A: LN1 + QKV (q, k scaled; rounded to T) ----------------------------------------------------------
@@ -624,7 +641,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 return;
             }
             stamp(l, 0, 0);
-            ln_rows<T, D>(xf, M, W.ln1_w, W.ln1_b, xs, lred, lnp);
+            ln_rows<T, D>(xf, M, lnp, lnp + D, xs, lred);
             __syncthreads();
             float acc[NCQ][MAXM];
             wq.template run<MAXM>(xs, D, M, acc);
@@ -677,7 +694,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         // ---- C: out projection + residual -----------------------------------------------------------------------
         {
             wxq.load(W.xq, W.bxq, D, D, true);
+            ln_issue(W.lnx_w, W.lnx_b);
             if (!sweep_xs(g_so, D / 2, tag(l, 2))) return;
+            ln_commit(2);  // (read after phase D's sweep barriers)
             stamp(l, 2, 0);
             float acc[NC1][MAXM];
             wo.template run<MAXM>(xs, D, M, acc);
@@ -698,7 +717,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
-            ln_rows<T, D>(xf, M, W.lnx_w, W.lnx_b, xs, lred, lnp);
+            ln_rows<T, D>(xf, M, lnp + 2 * D, lnp + 3 * D, xs, lred);
             wxo.load(W.xo, W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
             __syncthreads();
             float acc[NCX][MAXM];
@@ -768,7 +787,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- F: cross-out projection + residual -------------------------------------------------------------------
         {
+            ln_issue(W.ln2_w, W.ln2_b);
             if (!sweep_xs(g_xo, D / 2, tag(l, 5))) return;
+            ln_commit(4);
             stamp(l, 5, 0);
             wf1.load(W.f1, W.b1, 4 * D, D, true);  // streams under this phase's GEMV and phase G's wait
             float acc[NC1][MAXM];
@@ -790,7 +811,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             if (!sweep_xf(g_x2, tag(l, 6))) return;
             stamp(l, 6, 0);
-            ln_rows<T, D>(xf, M, W.ln2_w, W.ln2_b, xs, lred, lnp);
+            ln_rows<T, D>(xf, M, lnp + 4 * D, lnp + 5 * D, xs, lred);
             __syncthreads();
             float acc[NC4][MAXM];
             wf1.template run<MAXM>(xs, D, M, acc);
@@ -824,7 +845,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
         {
+            if (l + 1 < L) ln_issue(a.layers[l + 1].ln1_w, a.layers[l + 1].ln1_b);
+            else ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
             if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
+            ln_commit(0);
             stamp(l, 7, 0);
             if (l + 1 < L) wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);  // under the GEMV
             float acc[NC1][MAXM];
@@ -846,7 +870,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
     if (w0 == 0) {
         if (!sweep_xf(g_x0, tag(L, 0))) return;
-        ln_rows<T, D>(xf, M, a.lnd_w, a.lnd_b, (T*)a.out_dh, lred, lnp);
+        ln_rows<T, D>(xf, M, lnp, lnp + D, (T*)a.out_dh, lred);
     }
 }
 
