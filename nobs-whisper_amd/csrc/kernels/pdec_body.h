@@ -219,32 +219,39 @@ struct ColSlice {
             }
         }
     }
-    // acc[j][m] (all lanes) = sum_k xs[m][k] * W[c0 + wave + 4j][k]
+    // acc[j][m] (all lanes) = sum_k xs[m][k] * W[c0 + wave + 4j][k]. The rows' LDS vectors of a step are
+    // read unconditionally first (rows >= M and lanes past K read row 0 / vector 0: their weights are 0 or
+    // their sums unused), so the reads are not serialised behind per-row branches.
     template <int MAXM>
     __device__ __forceinline__ void run(const T* xs, int ldx, int M, float (&acc)[NCW][MAXM]) const {
-        const int wave = ptid() >> 6, lane = ptid() & 63;
+        const int lane = ptid() & 63;
 #pragma unroll
         for (int j = 0; j < NCW; j++)
 #pragma unroll
             for (int m = 0; m < MAXM; m++) acc[j][m] = 0.0f;
-        auto fma8 = [&](const float (&wf)[8], int j, int koff) {
+        auto fma8 = [&](const float (&wf)[8], int j, const u32x4 (&xv)[MAXM]) {
 #pragma unroll
             for (int m = 0; m < MAXM; m++) {
-                if (m >= M) break;
-                const u32x4 xv = *(const u32x4*)(xs + (long)m * ldx + koff);
-                const T* xe = (const T*)&xv;
-                float acc_ = acc[j][m];
+                if (m < M) {  // (uniform)
+                    const T* xe = (const T*)&xv[m];
+                    float acc_ = acc[j][m];
 #pragma unroll
-                for (int e = 0; e < 8; e++) acc_ = __builtin_fmaf((float)xe[e], wf[e], acc_);
-                acc[j][m] = acc_;
+                    for (int e = 0; e < 8; e++) acc_ = __builtin_fmaf((float)xe[e], wf[e], acc_);
+                    acc[j][m] = acc_;
+                }
             }
+        };
+        auto rows = [&](int koff, u32x4 (&xv)[MAXM]) {
+#pragma unroll
+            for (int m = 0; m < MAXM; m++) xv[m] = *(const u32x4*)(xs + (long)(m < M ? m : 0) * ldx + koff);
         };
         if (!Q) {
             const int nvec = K >> 3;
 #pragma unroll
             for (int v = 0; v < NV; v++) {
                 const int vi = lane + 64 * v;
-                if (vi >= nvec) break;
+                u32x4 xv[MAXM];
+                rows(vi < nvec ? vi * 8 : 0, xv);  // (lanes past K hold zero weights)
 #pragma unroll
                 for (int j = 0; j < NCW; j++) {
                     // one weight vector widened at a time (the prefetched weights stay packed in registers)
@@ -252,7 +259,7 @@ struct ColSlice {
                     const T* we = (const T*)&w[j][v];
 #pragma unroll
                     for (int e = 0; e < 8; e++) wf[e] = (float)we[e];
-                    fma8(wf, j, vi * 8);
+                    fma8(wf, j, xv);
                 }
             }
         } else {
@@ -260,7 +267,10 @@ struct ColSlice {
 #pragma unroll
             for (int v = 0; v < NB; v++) {
                 const int bi = lane + 64 * v;
-                if (bi >= nblk) break;
+                const int kb = bi < nblk ? bi * 32 : 0;  // (blocks past K: zero scales)
+                u32x4 xv[4][MAXM];
+#pragma unroll
+                for (int g = 0; g < 4; g++) rows(kb + g * 8, xv[g]);
 #pragma unroll
                 for (int j = 0; j < NCW; j++) {
                     const u32x4 a = w[j][2 * v], b = w[j][2 * v + 1], meta = w[j][2 * NB + v];
@@ -270,7 +280,7 @@ struct ColSlice {
                         const uint32_t b0 = qt == 8 ? (g < 2 ? a[2 * g] : b[2 * g - 4]) : a[2 * (g & 1)];
                         const uint32_t b1 = qt == 8 ? (g < 2 ? a[2 * g + 1] : b[2 * g - 3]) : a[2 * (g & 1) + 1];
                         deq8<T>(qt, b0, b1, meta.x, meta.y, g, wf);
-                        fma8(wf, j, bi * 32 + g * 8);
+                        fma8(wf, j, xv[g]);
                     }
                 }
             }
@@ -283,57 +293,69 @@ struct ColSlice {
 };
 
 // LayerNorm of rows [0, M <= 4) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
-// layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over wpr = 4 / M
+// layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over WPR = 4 / M
 // waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
-// per row; lane l of a row's wave q holds elements k = l + 64 (q + wpr e), re-read from LDS in each pass.
-// gamma / beta (gam, bet) are LDS copies staged by phase A (stage_ln in the kernel), off the critical path.
-template <typename T, int D>
-__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gam, const float* bet, T* out, double* lred) {
+// per row; lane l of a row's wave q holds elements k = l + 64 (q + WPR e), e < NE, all read from LDS at
+// once into registers (no branch per element: the reads are not serialised). gamma / beta (gam, bet)
+// are LDS copies staged a phase ahead (ln_issue / ln_commit in the kernel).
+template <typename T, int D, int WPR>
+__device__ __forceinline__ void ln_rows_w(const float* xf, int M, const float* gam, const float* bet, T* out, double* lred) {
 #pragma clang fp contract(off)
-    constexpr int NPL = (D + 63) / 64;
+    constexpr int NE = ((D + 63) / 64 + WPR - 1) / WPR;
     const int tid = ptid(), wave = tid >> 6, lane = tid & 63;
-    const int wpr = M == 1 ? 4 : (M == 2 ? 2 : 1);  // uniform
-    const int q = wave % wpr, m = wave / wpr;
+    const int q = wave % WPR, m = wave / WPR;
     const bool on = m < M;
-    const float* x = xf + (long)m * D;
+    const float* x = xf + (long)(on ? m : 0) * D;
+    float v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; e++) {
+        const int k = lane + 64 * (q + WPR * e);
+        const float xv = x[k < D ? k : 0];
+        v[e] = k < D ? xv : 0.0f;
+    }
     double s = 0.0;
 #pragma unroll
-    for (int e = 0; e < NPL; e++) {
-        const int k = lane + 64 * (q + wpr * e);
-        if (on && k < D) s += (double)x[k];
-    }
+    for (int e = 0; e < NE; e++) s += (double)v[e];
     s = wave_sum_d(s);
     if (lane == 0) lred[wave] = s;
     __syncthreads();
     double st = 0.0;
-    for (int i = 0; i < wpr; i++) st += lred[m * wpr + i];
+#pragma unroll
+    for (int i = 0; i < WPR; i++) st += lred[m * WPR + i];
     const float mean = (float)(st / D);
     double s2 = 0.0;
 #pragma unroll
-    for (int e = 0; e < NPL; e++) {
-        const int k = lane + 64 * (q + wpr * e);
-        if (on && k < D) {
-            const float v = x[k] - mean;
-            s2 += (double)(v * v);
-        }
+    for (int e = 0; e < NE; e++) {
+        const int k = lane + 64 * (q + WPR * e);
+        v[e] = v[e] - mean;
+        if (k < D) s2 += (double)(v[e] * v[e]);
     }
     s2 = wave_sum_d(s2);
     if (lane == 0) lred[4 + wave] = s2;
     __syncthreads();
     double st2 = 0.0;
-    for (int i = 0; i < wpr; i++) st2 += lred[4 + m * wpr + i];
+#pragma unroll
+    for (int i = 0; i < WPR; i++) st2 += lred[4 + m * WPR + i];
     const float variance = (float)(st2 / D);
     const float scale = 1.0f / sqrtf(variance + 1e-5f);
+    if (on) {
 #pragma unroll
-    for (int e = 0; e < NPL; e++) {
-        const int k = lane + 64 * (q + wpr * e);
-        if (on && k < D) {
-            float t = (x[k] - mean) * scale;
-            t = t * gam[k];
-            out[(long)m * D + k] = (T)(t + bet[k]);
+        for (int e = 0; e < NE; e++) {
+            const int k = lane + 64 * (q + WPR * e);
+            if (k < D) {
+                float t = v[e] * scale;
+                t = t * gam[k];
+                out[(long)m * D + k] = (T)(t + bet[k]);
+            }
         }
     }
     __syncthreads();  // lred is rewritten by the next call
+}
+template <typename T, int D>
+__device__ __forceinline__ void ln_rows(const float* xf, int M, const float* gam, const float* bet, T* out, double* lred) {
+    if (M == 1) ln_rows_w<T, D, 4>(xf, M, gam, bet, out, lred);
+    else if (M == 2) ln_rows_w<T, D, 2>(xf, M, gam, bet, out, lred);
+    else ln_rows_w<T, D, 1>(xf, M, gam, bet, out, lred);
 }
 
 // ---- hand-offs: data-tagged granules ----------------------------------------------------------------------
@@ -438,9 +460,14 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
                                           float* sc, float* red, float* res) {
     const int tid = ptid(), lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
     constexpr int NG = kNT / 8, CH = NG * U;
-    float qv[8];
+    // (branch-free per row: every LDS value is read up front, rows are selected, not branched on)
+    float qv[8], fkv[8], fvv[8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
+    for (int e = 0; e < 8; e++) {
+        qv[e] = qs[lane8 * 8 + e];
+        fkv[e] = fresh >= 0 ? fk[lane8 * 8 + e] : 0.0f;
+        fvv[e] = fresh >= 0 ? fv[lane8 * 8 + e] : 0.0f;
+    }
     float lmax = -INFINITY;
     for (int c0 = r0; c0 < (MULTI ? r1 : r0 + 1); c0 += CH) {
         if (c0 != r0) attn_rows<T, U>(K, c0, r1, fresh, rk);
@@ -448,19 +475,13 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
         for (int u = 0; u < U; u++) {
             const int t = c0 + grp + NG * u;
             const T* ke = (const T*)&rk[u];
+            const bool fr = t == fresh;
             float a = 0.0f;
-            if (t == fresh) {
 #pragma unroll
-                for (int e = 0; e < 8; e++) a += qv[e] * fk[lane8 * 8 + e];
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; e++) a += qv[e] * (float)ke[e];
-            }
+            for (int e = 0; e < 8; e++) a += qv[e] * (fr ? fkv[e] : (float)ke[e]);
             a = sum8(a);
-            if (t < r1) {
-                if (lane8 == 0) sc[t - r0] = a;
-                lmax = fmaxf(lmax, a);
-            }
+            if (t < r1 && lane8 == 0) sc[t - r0] = a;
+            lmax = t < r1 ? fmaxf(lmax, a) : lmax;
         }
     }
     lmax = wave_max(lmax);
@@ -480,19 +501,20 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
     auto pv = [&](int c0, const u32x4 (&r)[U]) {
+        float p[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = c0 + grp + NG * u;
-            if (t < r1) {
-                const float p = sc[t - r0];
-                if (t == fresh) {
+            p[u] = sc[t < r1 ? t - r0 : 0];
+        }
 #pragma unroll
-                    for (int e = 0; e < 8; e++) acc[e] += p * fv[lane8 * 8 + e];
-                } else {
-                    const T* ve = (const T*)&r[u];
+        for (int u = 0; u < U; u++) {
+            const int t = c0 + grp + NG * u;
+            if (t < r1) {  // (rows past the range: their V registers are zero, skipped all the same)
+                const bool fr = t == fresh;
+                const T* ve = (const T*)&r[u];
 #pragma unroll
-                    for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];
-                }
+                for (int e = 0; e < 8; e++) acc[e] += p[u] * (fr ? fvv[e] : (float)ve[e]);
             }
         }
     };
@@ -754,7 +776,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 4, 0);
-                attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, nullptr, nullptr, sc, red, res);
+                attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res);  // (no fresh row)
                 // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
                 // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
                 unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
