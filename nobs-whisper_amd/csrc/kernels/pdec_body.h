@@ -620,8 +620,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     wq.load(a.layers[0].qkv, a.layers[0].bqkv, 3 * D, D, true);
 
     // LayerNorm gamma / beta into lnp slots (LN1 at 0, 1; cross LN at 2, 3; LN2 at 4, 5): issued into
-    // registers before the wait of the phase ahead of the LayerNorm's phase (C for the cross LN, F for LN2,
-    // H for the next layer's LN1 or the final LN), so they land under that wait, and stored after it
+    // registers two phases ahead of the LayerNorm's phase (B for the cross LN, E for LN2, G for the next
+    // layer's LN1 or the final LN), stored after the next phase's wait (C, F, H)
     constexpr int NGL = (2 * D + kNT - 1) / kNT;
     float lv[NGL];
     auto ln_issue = [&](const float* gw, const float* gb) {
@@ -684,7 +684,15 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- B: self attention of (row, head) over the cache + this position (one task each) ----------------
         {
+            // phase C's and D's weights and D's LayerNorm parameters land under this phase: an attention
+            // workgroup (whose output everyone waits for) issues D's after its query arrived, so its wait
+            // is not behind them, and starts C with all of them in registers
             wo.load(W.o, W.bo, D, D, false);
+            auto ahead = [&] {
+                wxq.load(W.xq, W.bxq, D, D, true);
+                ln_issue(W.lnx_w, W.lnx_b);
+            };
+            if (w0 >= M * H) ahead();
             if (w0 < M * H) {
                 const int m = w0 / H, h = w0 % H;
                 const int pos = a.pos[m], nkv = pos + 1;
@@ -701,6 +709,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 1, 0);
+                ahead();
                 if (tid < 64) {  // append this position's k, v to the cache (read by the next steps' launches)
                     Kc[(long)pos * 64 + tid] = (T)qf[64 + tid];
                     Vc[(long)pos * 64 + tid] = (T)qf[128 + tid];
@@ -715,8 +724,6 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- C: out projection + residual -----------------------------------------------------------------------
         {
-            wxq.load(W.xq, W.bxq, D, D, true);
-            ln_issue(W.lnx_w, W.lnx_b);
             if (!sweep_xs(g_so, D / 2, tag(l, 2))) return;
             ln_commit(2);  // (read after phase D's sweep barriers)
             stamp(l, 2, 0);
@@ -759,7 +766,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- E: cross attention over the cached K/V, split over keys; split 0 of a (row, head) merges -----------
         {
+            auto ahead = [&] {  // phase G's weights and LayerNorm parameters (after the query, as in B)
+                ln_issue(W.ln2_w, W.ln2_b);
+                wf1.load(W.f1, W.b1, 4 * D, D, true);
+            };
             const int S = a.s_cross;
+            if (w0 >= M * H * S) ahead();
             if (w0 < M * H * S) {
                 const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
                 const int T_ = a.n_audio_ctx;
@@ -776,6 +788,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 4, 0);
+                ahead();
                 attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res);  // (no fresh row)
                 // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
                 // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
@@ -809,11 +822,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- F: cross-out projection + residual -------------------------------------------------------------------
         {
-            ln_issue(W.ln2_w, W.ln2_b);
             if (!sweep_xs(g_xo, D / 2, tag(l, 5))) return;
             ln_commit(4);
             stamp(l, 5, 0);
-            wf1.load(W.f1, W.b1, 4 * D, D, true);  // streams under this phase's GEMV and phase G's wait
             float acc[NC1][MAXM];
             wxo.template run<MAXM>(xs, D, M, acc);
 #pragma unroll
@@ -852,6 +863,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             }
             asm volatile("" ::: "memory");
             wf2.load(W.f2, W.b2, D, 4 * D, false);
+            if (l + 1 < L) {
+                wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);
+                ln_issue(a.layers[l + 1].ln1_w, a.layers[l + 1].ln1_b);
+            } else {
+                ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
+            }
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int j = 0; j < NC4; j++) {
@@ -867,12 +884,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
         {
-            if (l + 1 < L) ln_issue(a.layers[l + 1].ln1_w, a.layers[l + 1].ln1_b);
-            else ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
             if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
             ln_commit(0);
             stamp(l, 7, 0);
-            if (l + 1 < L) wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);  // under the GEMV
             float acc[NC1][MAXM];
             wf2.template run<MAXM>(xs, 4 * D, M, acc);
 #pragma unroll
