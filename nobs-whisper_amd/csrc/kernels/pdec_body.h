@@ -547,6 +547,21 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
     __syncthreads();
 }
 
+// The layer descriptors and the rows' token / position / slot are constant for the launch: read through
+// the constant address space they are scalar loads (lgkmcnt), which never wait behind the vector-memory
+// weight stream the way a vector load of a descriptor would (vmcnt retires in order).
+typedef __attribute__((address_space(4))) const PdecLayer CLayer;
+typedef __attribute__((address_space(4))) const PdecMat CMat;
+typedef __attribute__((address_space(4))) const int CInt;
+__device__ __forceinline__ PdecMat cmat(CMat& m) {
+    PdecMat r;
+    r.w = m.w;
+    r.qh = m.qh;
+    r.dm = m.dm;
+    r.qt = m.qt;
+    return r;
+}
+
 template <typename T, int D, int MAXM, bool Q>
 __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     constexpr int H = D / 64;
@@ -617,7 +632,11 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     ColSlice<T, NCX, NV1, Q> wxq;
     ColSlice<T, NC4, NV1, Q> wf1;
     ColSlice<T, NC1, NV4, Q> wf2;
-    wq.load(a.layers[0].qkv, a.layers[0].bqkv, 3 * D, D, true);
+    CLayer* LT = (CLayer*)a.layers;
+    CInt* TOK = (CInt*)a.tok;
+    CInt* POS = (CInt*)a.pos;
+    CInt* SLOT = (CInt*)a.slot;
+    wq.load(cmat(LT[0].qkv), LT[0].bqkv, 3 * D, D, true);
 
     // LayerNorm gamma / beta into lnp slots (LN1 at 0, 1; cross LN at 2, 3; LN2 at 4, 5): issued into
     // registers two phases ahead of the LayerNorm's phase (B for the cross LN, E for LN2, G for the next
@@ -638,17 +657,17 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             if (i < 2 * D) lnp[slot * D + i] = lv[u];
         }
     };
-    ln_issue(a.layers[0].ln1_w, a.layers[0].ln1_b);
+    ln_issue(LT[0].ln1_w, LT[0].ln1_b);
     ln_commit(0);
 
     for (int l = 0; l < L; l++) {
-        const PdecLayer& W = a.layers[l];
+        CLayer& W = LT[l];
         // ---- A: LN1 + QKV (q, k scaled; rounded to T) ----------------------------------------------------------
         {
             if (l == 0) {  // token + position embedding (embed_kernel's arithmetic)
                 for (int i = tid; i < M * D; i += kNT) {
                     const int m = i / D, k = i % D;
-                    const long t = a.tok[m], p = a.pos[m];
+                    const long t = TOK[m], p = POS[m];
                     xf[i] = (te32 ? te32[t * D + k] : (float)te[t * D + k]) + a.pos_d[p * D + k];
                 }
                 __syncthreads();
@@ -687,16 +706,16 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             // phase C's and D's weights and D's LayerNorm parameters land under this phase: an attention
             // workgroup (whose output everyone waits for) issues D's after its query arrived, so its wait
             // is not behind them, and starts C with all of them in registers
-            wo.load(W.o, W.bo, D, D, false);
+            wo.load(cmat(W.o), W.bo, D, D, false);
             auto ahead = [&] {
-                wxq.load(W.xq, W.bxq, D, D, true);
+                wxq.load(cmat(W.xq), W.bxq, D, D, true);
                 ln_issue(W.lnx_w, W.lnx_b);
             };
             if (w0 >= M * H) ahead();
             if (w0 < M * H) {
                 const int m = w0 / H, h = w0 % H;
-                const int pos = a.pos[m], nkv = pos + 1;
-                const long sl = a.slot[m];
+                const int pos = POS[m], nkv = pos + 1;
+                const long sl = SLOT[m];
                 T* Kc = (T*)self + (((sl * L + l) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
                 T* Vc = (T*)self + (((sl * L + l) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
                 u32x4 rk[16], rv[16];
@@ -747,7 +766,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
             ln_rows<T, D>(xf, M, lnp + 2 * D, lnp + 3 * D, xs, lred);
-            wxo.load(W.xo, W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
+            wxo.load(cmat(W.xo), W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
             __syncthreads();
             float acc[NCX][MAXM];
             wxq.template run<MAXM>(xs, D, M, acc);
@@ -768,7 +787,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             auto ahead = [&] {  // phase G's weights and LayerNorm parameters (after the query, as in B)
                 ln_issue(W.ln2_w, W.ln2_b);
-                wf1.load(W.f1, W.b1, 4 * D, D, true);
+                wf1.load(cmat(W.f1), W.b1, 4 * D, D, true);
             };
             const int S = a.s_cross;
             if (w0 >= M * H * S) ahead();
@@ -776,7 +795,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
                 const int T_ = a.n_audio_ctx;
                 const int r0 = (int)((long)s * T_ / S), r1 = (int)((long)(s + 1) * T_ / S);
-                const long sl = a.slot[m];
+                const long sl = SLOT[m];
                 const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
                 const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
                 u32x4 rk[8], rv[8];
@@ -862,10 +881,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 gt[j] = (lane < M && cl < wf1.nc) ? *gp(a.gelu_tab + __builtin_bit_cast(uint16_t, (half_t)gx[j])) : 0;
             }
             asm volatile("" ::: "memory");
-            wf2.load(W.f2, W.b2, D, 4 * D, false);
+            wf2.load(cmat(W.f2), W.b2, D, 4 * D, false);
             if (l + 1 < L) {
-                wq.load(a.layers[l + 1].qkv, a.layers[l + 1].bqkv, 3 * D, D, true);
-                ln_issue(a.layers[l + 1].ln1_w, a.layers[l + 1].ln1_b);
+                wq.load(cmat(LT[l + 1].qkv), LT[l + 1].bqkv, 3 * D, D, true);
+                ln_issue(LT[l + 1].ln1_w, LT[l + 1].ln1_b);
             } else {
                 ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
             }
