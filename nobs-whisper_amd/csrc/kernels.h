@@ -198,7 +198,7 @@ struct PdecLayer {
 // offset); R = kPdecMaxRows.
 struct PdecGranules {
     long x0, x1, x2, qkv, so, qx, xo, ff, part;
-    long err_bytes, bytes;
+    long err_bytes, zero_bytes, bytes;  // the error word; 256 zero bytes that no one writes (a zero page)
 };
 PdecGranules pdec_granules(int d, int L, int H);
 struct PdecArgs {

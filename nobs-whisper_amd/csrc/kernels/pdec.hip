@@ -37,7 +37,8 @@ PdecGranules pdec_granules(int d, int L, int H) {
     g.ff = o; o += R * 2 * d;
     g.part = o; o += (long)kG * 66;
     g.err_bytes = o * 8;
-    g.bytes = g.err_bytes + 16;
+    g.zero_bytes = g.err_bytes + 16;
+    g.bytes = g.zero_bytes + 256;
     return g;
 }
 

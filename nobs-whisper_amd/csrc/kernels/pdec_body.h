@@ -168,7 +168,9 @@ struct ColSlice {
     float bias[NCW];  // the bias of each of the lane's columns (loaded with the weights: no dependent load later)
     int c0, nc, K, qt;
     // pairs: slices of whole column pairs (2i, 2i + 1), for outputs handed off as packed T pairs
-    __device__ __forceinline__ void load(const PdecMat& W, const float* b, int N, int K_, bool pairs) {
+    // (every load is issued, lanes without data reading the zero page zp: a "cond ? load : 0" would
+    // make the register's zero write wait for the load last in flight into it)
+    __device__ __forceinline__ void load(const PdecMat& W, const float* b, int N, int K_, bool pairs, const void* zp) {
         K = K_;
         qt = Q ? W.qt : 0;
         const int w0 = blockIdx.x, u = pairs ? 2 : 1, nu = N / u;
@@ -176,7 +178,7 @@ struct ColSlice {
         nc = u * (int)((long)(w0 + 1) * nu / kG) - c0;
         const int wave = ptid() >> 6, lane = ptid() & 63;
 #pragma unroll
-        for (int j = 0; j < NCW; j++) bias[j] = wave + 4 * j < nc ? *gp(b + c0 + wave + 4 * j) : 0.0f;
+        for (int j = 0; j < NCW; j++) bias[j] = *gp(wave + 4 * j < nc ? b + c0 + wave + 4 * j : (const float*)zp);
         if (!Q) {
             const int nvec = K >> 3;
 #pragma unroll
@@ -186,8 +188,8 @@ struct ColSlice {
 #pragma unroll
                 for (int v = 0; v < NV; v++) {
                     const int vi = lane + 64 * v;
-                    w[j][v] = (cl < nc && vi < nvec) ? __builtin_nontemporal_load(gp((const u32x4*)(row + vi * 8)))
-                                                     : (u32x4){0, 0, 0, 0};
+                    const T* src = (cl < nc && vi < nvec) ? row + vi * 8 : (const T*)zp;
+                    w[j][v] = __builtin_nontemporal_load(gp((const u32x4*)src));
                 }
             }
             return;
@@ -201,18 +203,18 @@ struct ColSlice {
 #pragma unroll
             for (int v = 0; v < NB; v++) {
                 const int bi = lane + 64 * v;
-                u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0}, meta = {0, 0, 0, 0};
-                if (cl < nc && bi < nblk) {
-                    const long blk = n * nblk + bi;
-                    if (qt == 8) {
-                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi)));
-                        b = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * K + 32L * bi + 16)));
-                    } else {
-                        a = __builtin_nontemporal_load(gp((const u32x4*)(qs + n * (K / 2) + 16L * bi)));
-                    }
-                    meta.x = (qt == 6 || qt == 7) ? *gp(W.qh + blk) : 0u;
-                    meta.y = (qt == 3 || qt == 7) ? *gp((const uint32_t*)W.dm + blk) : (uint32_t)*gp(W.dm + blk);
-                }
+                const bool in = cl < nc && bi < nblk;
+                const long blk = n * nblk + (in ? bi : 0);
+                const uint8_t* pa = !in ? (const uint8_t*)zp : (qt == 8 ? qs + n * K + 32L * bi : qs + n * (K / 2) + 16L * bi);
+                const uint8_t* pb = (in && qt == 8) ? pa + 16 : (const uint8_t*)zp;
+                const bool q5 = qt == 6 || qt == 7, wide = qt == 3 || qt == 7;  // (uniform)
+                const u32x4 a = __builtin_nontemporal_load(gp((const u32x4*)pa));
+                const u32x4 b = __builtin_nontemporal_load(gp((const u32x4*)pb));
+                u32x4 meta;
+                meta.x = *gp((in && q5) ? W.qh + blk : (const uint32_t*)zp);
+                meta.y = wide ? *gp(in ? (const uint32_t*)W.dm + blk : (const uint32_t*)zp)
+                              : (uint32_t)*gp(in ? W.dm + blk : (const uint16_t*)zp);
+                meta.z = meta.w = 0;
                 w[j][2 * v] = a;
                 w[j][2 * v + 1] = b;
                 w[j][2 * NB + v] = meta;
@@ -438,26 +440,25 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, int n, unsign
 // chunk's keys are scored (MULTI; a task of one chunk compiles without the loops). Leaves in res (LDS): o[64] = sum_t p_t v_t, res[64] = max score, res[65] =
 // sum_t p_t, with p_t = e^(s_t - max) (rounded to T as the P.V operand).
 template <typename T, int U>
-__device__ __forceinline__ void attn_rows(const T* __restrict__ X, int t0, int r1, int fresh, u32x4 (&r)[U]) {
+__device__ __forceinline__ void attn_rows(const T* __restrict__ X, int t0, int r1, int fresh, u32x4 (&r)[U], const void* zp) {
     const int lane8 = ptid() & 7, grp = ptid() >> 3;
     constexpr int NG = kNT / 8;
-    const u32x4 zero = {0, 0, 0, 0};
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < U; u++) {  // (rows out of range read the zero page: every load is issued)
         const int t = t0 + grp + NG * u;
-        r[u] = (t < r1 && t != fresh) ? *gp((const u32x4*)(X + (long)t * 64 + lane8 * 8)) : zero;
+        r[u] = *gp((const u32x4*)((t < r1 && t != fresh) ? X + (long)t * 64 + lane8 * 8 : (const T*)zp));
     }
 }
 template <typename T, int U>
 __device__ __forceinline__ void attn_load(const T* __restrict__ K, const T* __restrict__ V, int r0, int r1, int fresh,
-                                          u32x4 (&rk)[U], u32x4 (&rv)[U]) {
-    attn_rows<T, U>(K, r0, r1, fresh, rk);
-    attn_rows<T, U>(V, r0, r1, fresh, rv);
+                                          u32x4 (&rk)[U], u32x4 (&rv)[U], const void* zp) {
+    attn_rows<T, U>(K, r0, r1, fresh, rk, zp);
+    attn_rows<T, U>(V, r0, r1, fresh, rv, zp);
 }
 template <typename T, int U, bool MULTI>
 __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__ K, const T* __restrict__ V, u32x4 (&rk)[U],
                                           const u32x4 (&rv)[U], int r0, int r1, int fresh, const float* fk, const float* fv,
-                                          float* sc, float* red, float* res) {
+                                          float* sc, float* red, float* res, const void* zp) {
     const int tid = ptid(), lane8 = tid & 7, grp = tid >> 3, wave = tid >> 6, lane = tid & 63;
     constexpr int NG = kNT / 8, CH = NG * U;
     // (branch-free per row: every LDS value is read up front, rows are selected, not branched on)
@@ -470,7 +471,7 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
     }
     float lmax = -INFINITY;
     for (int c0 = r0; c0 < (MULTI ? r1 : r0 + 1); c0 += CH) {
-        if (c0 != r0) attn_rows<T, U>(K, c0, r1, fresh, rk);
+        if (c0 != r0) attn_rows<T, U>(K, c0, r1, fresh, rk, zp);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = c0 + grp + NG * u;
@@ -520,7 +521,7 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
     };
     pv(r0, rv);
     for (int c0 = r0 + CH; MULTI && c0 < r1; c0 += CH) {
-        attn_rows<T, U>(V, c0, r1, fresh, rk);
+        attn_rows<T, U>(V, c0, r1, fresh, rk, zp);
         pv(c0, rk);
     }
     // reduce over the 8 groups of a wave (lanes lane8 + 8 g): DPP for xor 8, permutes for 16 and 32; then over the 4 waves in LDS
@@ -592,6 +593,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     unsigned long long *g_so = gb + G.so, *g_qx = gb + G.qx, *g_xo = gb + G.xo, *g_ff = gb + G.ff;
     unsigned long long* g_part = gb + G.part;
     unsigned* err = (unsigned*)((char*)a.sync + G.err_bytes);
+    const void* zp = (const char*)a.sync + G.zero_bytes;  // 256 zero bytes (zeroed per launch, never written)
     const T* te = (const T*)a.tok_emb;
     const float* te32 = a.te_f32 ? (const float*)a.tok_emb : nullptr;
     const T* self = (const T*)a.self_cache;
@@ -636,7 +638,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     CInt* TOK = (CInt*)a.tok;
     CInt* POS = (CInt*)a.pos;
     CInt* SLOT = (CInt*)a.slot;
-    wq.load(cmat(LT[0].qkv), LT[0].bqkv, 3 * D, D, true);
+    wq.load(cmat(LT[0].qkv), LT[0].bqkv, 3 * D, D, true, zp);
 
     // LayerNorm gamma / beta into lnp slots (LN1 at 0, 1; cross LN at 2, 3; LN2 at 4, 5): issued into
     // registers two phases ahead of the LayerNorm's phase (B for the cross LN, E for LN2, G for the next
@@ -647,7 +649,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
 #pragma unroll
         for (int u = 0; u < NGL; u++) {
             const int i = tid + kNT * u;
-            lv[u] = i < D ? *gp(gw + i) : (i < 2 * D ? *gp(gb + (i - D)) : 0.0f);
+            const int ii = i < 2 * D ? i : 2 * D - 1;  // (2d is a multiple of 256 for every d built)
+            lv[u] = *gp(ii < D ? gw + ii : gb + (ii - D));
         }
     };
     auto ln_commit = [&](int slot) {
@@ -706,9 +709,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             // phase C's and D's weights and D's LayerNorm parameters land under this phase: an attention
             // workgroup (whose output everyone waits for) issues D's after its query arrived, so its wait
             // is not behind them, and starts C with all of them in registers
-            wo.load(cmat(W.o), W.bo, D, D, false);
+            wo.load(cmat(W.o), W.bo, D, D, false, zp);
             auto ahead = [&] {
-                wxq.load(cmat(W.xq), W.bxq, D, D, true);
+                wxq.load(cmat(W.xq), W.bxq, D, D, true, zp);
                 ln_issue(W.lnx_w, W.lnx_b);
             };
             if (w0 >= M * H) ahead();
@@ -719,7 +722,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 T* Kc = (T*)self + (((sl * L + l) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
                 T* Vc = (T*)self + (((sl * L + l) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
                 u32x4 rk[16], rv[16];
-                attn_load<T, 16>(Kc, Vc, 0, nkv, pos, rk, rv);  // the cached rows land while the query is awaited
+                attn_load<T, 16>(Kc, Vc, 0, nkv, pos, rk, rv, zp);  // the cached rows land while the query is awaited
                 // q, k, v of head h: granules h * 32 + i of each third of the row
                 if (!sweep(g_qkv, 96, tag(l, 1), [&](int i) { return (long)m * (3 * D / 2) + (i >> 5) * (D / 2) + h * 32 + (i & 31); },
                            [&](int i, uint32_t b) {
@@ -733,7 +736,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     Kc[(long)pos * 64 + tid] = (T)qf[64 + tid];
                     Vc[(long)pos * 64 + tid] = (T)qf[128 + tid];
                 }
-                attn_task<T, 16, false>(qf, Kc, Vc, rk, rv, 0, nkv, pos, qf + 64, qf + 128, sc, red, res);
+                attn_task<T, 16, false>(qf, Kc, Vc, rk, rv, 0, nkv, pos, qf + 64, qf + 128, sc, red, res, zp);
                 if (tid < 32) {
                     const float inv = 1.0f / res[65];
                     put_g(g_so, (long)m * (D / 2) + h * 32 + tid, tag(l, 2), pack2<T>(res[2 * tid] * inv, res[2 * tid + 1] * inv));
@@ -766,10 +769,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             if (!sweep_xf(g_x1, tag(l, 3))) return;
             stamp(l, 3, 0);
             ln_rows<T, D>(xf, M, lnp + 2 * D, lnp + 3 * D, xs, lred);
-            wxo.load(cmat(W.xo), W.bxo, D, D, false);  // after the LayerNorm's gamma / beta loads
             __syncthreads();
             float acc[NCX][MAXM];
             wxq.template run<MAXM>(xs, D, M, acc);
+            wxo.load(cmat(W.xo), W.bxo, D, D, false, zp);  // (after the GEMV: its operand waits are not behind it)
 #pragma unroll
             for (int j = 0; j < NCX; j++)
 #pragma unroll
@@ -787,7 +790,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         {
             auto ahead = [&] {  // phase G's weights and LayerNorm parameters (after the query, as in B)
                 ln_issue(W.ln2_w, W.ln2_b);
-                wf1.load(cmat(W.f1), W.b1, 4 * D, D, true);
+                wf1.load(cmat(W.f1), W.b1, 4 * D, D, true, zp);
             };
             const int S = a.s_cross;
             if (w0 >= M * H * S) ahead();
@@ -799,7 +802,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
                 const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
                 u32x4 rk[8], rv[8];
-                attn_load<T, 8>(Kc, Vc, r0, r1, -1, rk, rv);  // constant for the window: issued before the wait
+                attn_load<T, 8>(Kc, Vc, r0, r1, -1, rk, rv, zp);  // constant for the window: issued before the wait
                 if (!sweep(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
                            [&](int i, uint32_t b) {
                                qf[2 * i] = (float)lo_t<T>(b);
@@ -808,7 +811,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     return;
                 stamp(l, 4, 0);
                 ahead();
-                attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res);  // (no fresh row)
+                attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res, zp);  // (no fresh row)
                 // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
                 // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
                 unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
@@ -878,12 +881,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
 #pragma unroll
                 for (int m = 0; m < MAXM; m++)
                     if (lane == m) gx[j] = acc[j][m] + wf1.bias[j];
-                gt[j] = (lane < M && cl < wf1.nc) ? *gp(a.gelu_tab + __builtin_bit_cast(uint16_t, (half_t)gx[j])) : 0;
+                gt[j] = *gp(a.gelu_tab + ((lane < M && cl < wf1.nc) ? __builtin_bit_cast(uint16_t, (half_t)gx[j]) : 0));
             }
             asm volatile("" ::: "memory");
-            wf2.load(cmat(W.f2), W.b2, D, 4 * D, false);
+            wf2.load(cmat(W.f2), W.b2, D, 4 * D, false, zp);
             if (l + 1 < L) {
-                wq.load(cmat(LT[l + 1].qkv), LT[l + 1].bqkv, 3 * D, D, true);
+                wq.load(cmat(LT[l + 1].qkv), LT[l + 1].bqkv, 3 * D, D, true, zp);
                 ln_issue(LT[l + 1].ln1_w, LT[l + 1].ln1_b);
             } else {
                 ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
