@@ -349,7 +349,8 @@ __global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-// attn_enc2_kernel software-pipelined across key tiles (WHISPER_MI355X_ATTN=3): iteration t issues the
+// attn_enc2_kernel software-pipelined across key tiles (variant 3 of whisper_mi355x_bench_attn_encoder;
+// measured slower, kept bit-identical under test): iteration t issues the
 // score MFMAs of tile t+1 first, then runs the softmax of tile t and its P.V MFMAs, so a wave has
 // independent MFMA work in flight under its exponentials instead of alternating MFMA-only and
 // VALU-only phases in lockstep with its SIMD partner. K runs one tile ahead of V in the same two LDS
