@@ -9,7 +9,9 @@ all with the "+conf" decoders (make_model.CONF_SCALE) so windows end the way a t
 
 (a) f16 whisper_full (the reference's FullParams, whisper.rs:88-124, greedy attempt only:
     temperature_inc 0) on two clips per shape, in both cross-attention forms: token ids,
-    timestamps, segment text and per-window decisions identical to the oracle.
+    timestamps, segment text and per-window decisions identical to the oracle, up to the first oracle
+    near tie (F16_GAP, the rule of every f16 whisper_full test): large-v3-turbo clip 1 has a step the
+    oracle decides by 0.0049 nats, where the persistent step (cache form, 1 clip) took the other token.
 (b) BASELINE configs[3]'s own workload (bench.py's step): large-v3 at 128 clips in one batch, the
     direct cross form with the bench's split count, fixed-work mode (128 tokens per clip, EOT
     suppressed), every clip teacher-forced along the oracle's greedy sequence of a spot clip
@@ -28,12 +30,17 @@ import numpy as np
 import pytest
 
 from make_model import synthetic_pcm
+from margin_gate import assert_diverges_only_at_close_calls, kept_token_margins
 from oracle_py import Oracle, reference_params
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 F16_REL_TOL = 1e-3
 BF16_DEEP_TOL = 2.0
+# (a): exact where the oracle decided every greedy step by more than F16_GAP nats, else exact up to the
+# first such near tie: the rule of every f16 whisper_full test (tests/test_gpu_pdec.py);
+# f16 teacher-forced logits sit within ~0.015 of the oracle's
+F16_GAP = 0.05
 N_TOK = 128
 N_CLIPS = 128
 SPOT = (0, 41, 86, 127)
@@ -87,12 +94,18 @@ def test_full_depth_f16_exact(wrs, monkeypatch, shape, clip, cross):
     st.close()
     ctx.close()
     exp = [(s["tokens"], s["t0"], s["t1"]) for s in ref["segments"]]
-    assert _ints(segs) == exp
-    assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
-    keys = ("seek", "temp_idx", "failed0", "logprob_fail0", "result_len0", "no_speech")
-    assert [tuple(d[k] for k in keys) for d in dec] == [tuple(d[k] for k in keys) for d in ref["decisions"]]
-    print(f"{shape} clip {clip} {cross}: {sum(len(s['tokens']) for s in ref['segments'])} tokens identical "
-          f"over {len(ref['decisions'])} window(s)")
+    kept, margins = kept_token_margins(ref)
+    if min(margins) > F16_GAP:
+        assert _ints(segs) == exp
+        assert [s.text for s in segs] == [s["text"] for s in ref["segments"]]
+        keys = ("seek", "temp_idx", "failed0", "logprob_fail0", "result_len0", "no_speech")
+        assert [tuple(d[k] for k in keys) for d in dec] == [tuple(d[k] for k in keys) for d in ref["decisions"]]
+        print(f"{shape} clip {clip} {cross}: {sum(len(s['tokens']) for s in ref['segments'])} tokens identical "
+              f"over {len(ref['decisions'])} window(s)")
+    else:  # the oracle decided a step by <= F16_GAP nats: exact up to the first such near tie
+        got = [t for sg in _ints(segs) for t in sg[0]]
+        k = assert_diverges_only_at_close_calls(got, kept, margins, F16_GAP, 4)
+        print(f"{shape} clip {clip} {cross}: {k} of {len(kept)} tokens identical (oracle near tie {min(margins):.4f} nats)")
 
 
 # ---- (b) large-v3, 128 clips, direct form, fixed work, teacher-forced -----------------------------------
