@@ -201,6 +201,35 @@ struct PdecGranules {
     long err_bytes, zero_bytes, bytes;  // the error word; 256 zero bytes that no one writes (a zero page)
 };
 PdecGranules pdec_granules(int d, int L, int H);
+// LDS layout of one workgroup (byte offsets, 16-aligned), shared by the launcher and the kernel: rows are
+// provisioned for the launch's clip count when it is 1 or 2 (those launches also hold the |x| < 10 part
+// of ggml's f16 GELU table, 2 x 0x4900 entries), else for kPdecMaxRows
+struct PdecLds {
+    int xs, xf, sc, red, qf, res, ost, lred, lnp, part, lflag, gtab, bytes, rows, cmax;
+};
+constexpr int kPdecGeluHalf = 0x4900;  // f16 bit patterns below 10.0 (one sign)
+__host__ __device__ inline PdecLds pdec_lds(int d, int M, int S) {
+    auto up = [](int b) { return (b + 15) & ~15; };
+    PdecLds l{};
+    l.rows = M <= 2 ? M : kPdecMaxRows;
+    const int c1 = 2 * ((3 * d / 2 + 255) / 256), c4 = 2 * ((2 * d + 255) / 256);
+    l.cmax = c1 > c4 ? c1 : c4;
+    int o = 0;
+    l.xs = o; o += up(l.rows * 4 * d * 2);
+    l.xf = o; o += up(l.rows * d * 4);
+    l.sc = o; o += 1536 * 4;
+    l.red = o; o += up((8 + 256) * 4);
+    l.qf = o; o += 192 * 4;
+    l.res = o; o += up(68 * 4);
+    l.ost = o; o += up(l.rows * l.cmax * 4);
+    l.lred = o; o += 8 * 8;
+    l.lnp = o; o += up(6 * d * 4);
+    l.part = o; o += up(S * 66 * 4);
+    l.lflag = o; o += 16;
+    l.gtab = o; o += M <= 2 ? up(2 * kPdecGeluHalf * 2) : 0;
+    l.bytes = o;
+    return l;
+}
 struct PdecArgs {
     const PdecLayer* layers;  // device array [L]
     int L, M, d, n_text_ctx, n_audio_ctx;

@@ -48,13 +48,11 @@ void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
     if (a.M < 1 || a.M > kPdecMaxRows) WM_FAIL("pdec: %d rows", a.M);
     if (a.M * (a.d / 64) * a.s_cross > kG) WM_FAIL("pdec: split count");
     // self attention in one chunk (16 rows per lane group); cross-attention tasks of at most 1536 rows (the
-    // scores buffer); the cross partials of a (clip, head) fit the LDS rows buffer of the merging workgroup
-    if (a.n_text_ctx > 16 * kNT / 8 || (a.n_audio_ctx + a.s_cross - 1) / a.s_cross > 1536 ||
-        (size_t)a.s_cross * 66 * 4 > (size_t)kPdecMaxRows * 4 * a.d * 2)
-        WM_FAIL("pdec: context sizes");
-    const int CMAX = std::max(2 * ((3 * a.d / 2 + kG - 1) / kG), 2 * ((2 * a.d + kG - 1) / kG));
-    const size_t lds = (size_t)kPdecMaxRows * 4 * a.d * 2 + (size_t)kPdecMaxRows * a.d * 4 +
-                       (1536 + 8 + 256 + 192 + 68 + kPdecMaxRows * CMAX + 16 + 6 * (size_t)a.d + 4) * sizeof(float);
+    // scores buffer)
+    if (a.n_text_ctx > 16 * kNT / 8 || (a.n_audio_ctx + a.s_cross - 1) / a.s_cross > 1536) WM_FAIL("pdec: context sizes");
+    const PdecLds ll = pdec_lds(a.d, a.M, a.s_cross);
+    if (ll.bytes > 160 * 1024) WM_FAIL("pdec: %d bytes of LDS", ll.bytes);
+    const size_t lds = ll.bytes;
     WM_CHECK(hipMemsetAsync(a.sync, 0, a.gr.bytes, st));
     if (a.quant) {
         if (dt != DType::F16) WM_FAIL("pdec: GGML blocks with a bf16 context");

@@ -573,18 +573,22 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     constexpr int C1 = (D + kG - 1) / kG;
     constexpr int CQ = 2 * ((3 * D / 2 + kG - 1) / kG), CX = 2 * ((D / 2 + kG - 1) / kG), C4 = 2 * ((2 * D + kG - 1) / kG);
     constexpr int NC1 = (C1 + 3) / 4, NCQ = (CQ + 3) / 4, NCX = (CX + 3) / 4, NC4 = (C4 + 3) / 4;
-    constexpr int CMAX = std::max(CQ, C4);
+    constexpr int CMAX = std::max(CQ, C4);  // (== PdecLds::cmax)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* xs = (T*)smem;                                                 // [M][4d] T: the projections' rows
-    float* xf = (float*)(smem + (size_t)MAXM * 4 * D * sizeof(T));    // [M][d] f32: a handed-off x row
-    float* sc = xf + MAXM * D;                                        // scores [1536]
-    float* red = sc + 1536;                                           // [8 + 256]
-    float* qf = red + 8 + 256;                                        // q, fresh k, fresh v [3][64]
-    float* res = qf + 192;                                            // attention result [64 + 2] (+ pad)
-    float* ost = res + 68;                                            // packed outputs [M][CMAX]
-    double* lred = (double*)(ost + MAXM * CMAX);                      // LayerNorm partial sums [8]
-    float* lnp = (float*)(lred + 8);                                  // LayerNorm gamma, beta [6][d]
-    int* lflag = (int*)(lnp + 6 * D);
+    const PdecLds LL = pdec_lds(D, a.M, a.s_cross);
+    T* xs = (T*)(smem + LL.xs);              // [rows][4d] T: the projections' rows
+    float* xf = (float*)(smem + LL.xf);      // [rows][d] f32: a handed-off x row
+    float* sc = (float*)(smem + LL.sc);      // scores [1536]
+    float* red = (float*)(smem + LL.red);    // [8 + 256]
+    float* qf = (float*)(smem + LL.qf);      // q, fresh k, fresh v [3][64]
+    float* res = (float*)(smem + LL.res);    // attention result [64 + 2]
+    float* ost = (float*)(smem + LL.ost);    // packed outputs [rows][CMAX]
+    double* lred = (double*)(smem + LL.lred);  // LayerNorm partial sums [8]
+    float* lnp = (float*)(smem + LL.lnp);    // LayerNorm gamma, beta [6][d]
+    float* part = (float*)(smem + LL.part);  // the cross partials a merging workgroup gathers [S][66]
+    int* lflag = (int*)(smem + LL.lflag);
+    uint16_t* gtab = (uint16_t*)(smem + LL.gtab);  // GELU table, |x| < 10 (1-2 clips only)
+    const bool ltab = a.M <= 2;
 
     const int M = a.M, L = a.L, w0 = blockIdx.x, tid = ptid(), wave = tid >> 6, lane = tid & 63;
     const PdecGranules& G = a.gr;
@@ -662,6 +666,20 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     };
     ln_issue(LT[0].ln1_w, LT[0].ln1_b);
     ln_commit(0);
+    if (ltab) {  // ggml's f16 GELU table, the |x| < 10 bit patterns of each sign, into LDS
+        constexpr int NV = 2 * kPdecGeluHalf * 2 / 16;  // 16-byte vectors
+        u32x4 t[(NV + kNT - 1) / kNT];
+#pragma unroll
+        for (int u = 0; u < (NV + kNT - 1) / kNT; u++) {
+            const int i = tid + kNT * u, half = i >= NV / 2, j = i - half * (NV / 2);
+            t[u] = *gp((const u32x4*)(a.gelu_tab + (half ? 0x8000 : 0)) + (i < NV ? j : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < (NV + kNT - 1) / kNT; u++) {
+            const int i = tid + kNT * u;
+            if (i < NV) ((u32x4*)gtab)[i] = t[u];
+        }
+    }
 
     for (int l = 0; l < L; l++) {
         CLayer& W = LT[l];
@@ -818,7 +836,6 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 if (s > 0) {
                     if (tid < kPartG) put_g(gp0 + (long)s * kPartG, tid, tag(l, 4), __builtin_bit_cast(uint32_t, res[tid]));
                 } else {
-                    float* part = (float*)xs;  // [S][66] (xs is free until phase F's sweep)
                     if (tid < kPartG) part[tid] = res[tid];
                     if (!sweep<16>(gp0 + kPartG, (S - 1) * kPartG, tag(l, 4), [](int i) { return (long)i; },
                                    [&](int i, uint32_t b) { part[kPartG + i] = f32_of(b); }, err, lflag, spin))
@@ -837,7 +854,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                     __syncthreads();
                     if (tid < 32) put_g(g_xo, (long)m * (D / 2) + h * 32 + tid, tag(l, 5), pack2<T>(res[2 * tid], res[2 * tid + 1]));
-                    __syncthreads();  // part (in xs) read before phase F's sweep writes xs
+                    __syncthreads();  // part read before the next layer's merge rewrites it
                 }
                 stamp(l, 4, 1);
             }
@@ -881,7 +898,10 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
 #pragma unroll
                 for (int m = 0; m < MAXM; m++)
                     if (lane == m) gx[j] = acc[j][m] + wf1.bias[j];
-                gt[j] = *gp(a.gelu_tab + ((lane < M && cl < wf1.nc) ? __builtin_bit_cast(uint16_t, (half_t)gx[j]) : 0));
+                const unsigned hb = (lane < M && cl < wf1.nc) ? __builtin_bit_cast(uint16_t, (half_t)gx[j]) : 0u;
+                const unsigned hq = hb & 0x7FFF;
+                if (ltab && hq < kPdecGeluHalf) gt[j] = gtab[hq + (hb >> 15) * kPdecGeluHalf];  // (|x| < 10)
+                else gt[j] = *gp(a.gelu_tab + hb);
             }
             asm volatile("" ::: "memory");
             wf2.load(cmat(W.f2), W.b2, D, 4 * D, false, zp);
