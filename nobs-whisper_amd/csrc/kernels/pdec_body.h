@@ -91,12 +91,18 @@ __device__ __forceinline__ float sum8(float a) {
 __device__ __forceinline__ float lane_f(float x, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dppf_rows(float x) {  // rows outside the ROWS mask read 0
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROWS, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float x) {
     x += dppf<0xB1>(x);
     x += dppf<0x4E>(x);
     x += dppf<0x141>(x);
-    x += dppf<0x140>(x);
-    return (lane_f(x, 0) + lane_f(x, 16)) + (lane_f(x, 32) + lane_f(x, 48));
+    x += dppf<0x140>(x);  // every lane: its row's sum r_i
+    x += dppf_rows<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3: r0 + r1, r2 + r3
+    x += dppf_rows<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3: lane 63 = (r2 + r3) + (r0 + r1)
+    return lane_f(x, 63);
 }
 __device__ __forceinline__ float wave_max(float x) {
     x = fmaxf(x, dppf<0xB1>(x));
@@ -288,9 +294,11 @@ struct ColSlice {
             }
         }
 #pragma unroll
-        for (int j = 0; j < NCW; j++)
+        for (int m = 0; m < MAXM; m++)
+            if (m < M) {  // (uniform; the column chains of a row interleave)
 #pragma unroll
-            for (int m = 0; m < MAXM; m++) acc[j][m] = wave_sum(acc[j][m]);  // (branch-free: the chains interleave)
+                for (int j = 0; j < NCW; j++) acc[j][m] = wave_sum(acc[j][m]);
+            }
     }
 };
 
