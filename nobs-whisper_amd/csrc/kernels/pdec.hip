@@ -7,9 +7,12 @@
 
 namespace wm {
 
-void pdec_launch_f16(const PdecArgs& a, size_t lds, hipStream_t st);
-void pdec_launch_bf16(const PdecArgs& a, size_t lds, hipStream_t st);
-void pdec_launch_q(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_f16_1(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_bf16_1(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_q_1(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_f16_4(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_bf16_4(const PdecArgs& a, size_t lds, hipStream_t st);
+void pdec_launch_q_4(const PdecArgs& a, size_t lds, hipStream_t st);
 
 namespace {
 constexpr int kG = 256, kNT = 256;
@@ -54,13 +57,14 @@ void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
     if (ll.bytes > 160 * 1024) WM_FAIL("pdec: %d bytes of LDS", ll.bytes);
     const size_t lds = ll.bytes;
     WM_CHECK(hipMemsetAsync(a.sync, 0, a.gr.bytes, st));
+    const bool one = a.M == 1;  // the one-row build (the app's one clip per call)
     if (a.quant) {
         if (dt != DType::F16) WM_FAIL("pdec: GGML blocks with a bf16 context");
-        pdec_launch_q(a, lds, st);
+        one ? pdec_launch_q_1(a, lds, st) : pdec_launch_q_4(a, lds, st);
     } else if (dt == DType::F16) {
-        pdec_launch_f16(a, lds, st);
+        one ? pdec_launch_f16_1(a, lds, st) : pdec_launch_f16_4(a, lds, st);
     } else {
-        pdec_launch_bf16(a, lds, st);
+        one ? pdec_launch_bf16_1(a, lds, st) : pdec_launch_bf16_4(a, lds, st);
     }
 }
 

@@ -1,6 +1,7 @@
-// Persistent decode step, bf16_t plain weights (one translation unit per instantiation set: they build in parallel)
+// Persistent decode step, bf16_t plain weights, built for 4 rows (one translation unit per
+// instantiation set: they build in parallel)
 #include "pdec_body.h"
 
 namespace wm {
-void pdec_launch_bf16(const PdecArgs& a, size_t lds, hipStream_t st) { pdec_launch_t<bf16_t, false>(a, lds, st); }
+void pdec_launch_bf16_4(const PdecArgs& a, size_t lds, hipStream_t st) { pdec_launch_t<bf16_t, false, 4>(a, lds, st); }
 }  // namespace wm

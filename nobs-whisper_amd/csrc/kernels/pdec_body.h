@@ -962,11 +962,13 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
 
 // one launcher per (compute type, weight form); the GGML-block form is built for the catalog's quantized
 // shapes (small 768, medium 1024, large-v3 1280)
-template <typename T, bool Q>
+// MAXM: the rows the kernel's register arrays and unrolled loops are built for (1 for the app's one clip
+// per call: a much smaller loop body, 4 otherwise)
+template <typename T, bool Q, int MAXM>
 void pdec_launch_t(const PdecArgs& a, size_t lds, hipStream_t st) {
 #define WM_PD(DD)                                                        \
     case DD:                                                            \
-        pdec_kernel<T, DD, kPdecMaxRows, Q><<<kG, kNT, lds, st>>>(a);   \
+        pdec_kernel<T, DD, MAXM, Q><<<kG, kNT, lds, st>>>(a);           \
         return;
     if constexpr (!Q) {
         switch (a.d) { WM_PD(384) WM_PD(512) default: break; }
