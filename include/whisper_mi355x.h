@@ -131,6 +131,9 @@ WHISPER_API void whisper_mi355x_set_pdec_spin(long ticks);
  * from now on fill with the 100 MHz clock (per workgroup, layer and phase: input arrived, phase
  * signalled); NULL turns it off. */
 WHISPER_API void whisper_mi355x_set_pdec_stamps(void * dev);
+/* Quantized files: 1 = persistent decode steps stream the GGML blocks; 0 (default) = they read the
+ * context's expanded compute-type copy once it exists (faster). */
+WHISPER_API void whisper_mi355x_set_pdec_blocks(int on);
 /* Debug/tuning: the decode-step residual GEMM with its fused LayerNorm (M <= 128):
  * x[M][N] (f32, in/out) += A.B^T + bias, then y[M][N] (compute dtype) = LN(x) * ln_w + ln_b. */
 // fp8 (OCP e4m3) GEMM with per-row f32 scales (A per row m, B per row n), then epilogue `epi`;

@@ -555,6 +555,7 @@ void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
 void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
 void whisper_mi355x_set_pdec_spin(long ticks) { wm::g_pdec_spin_ticks = ticks; }
 void whisper_mi355x_set_pdec_stamps(void* dev) { wm::g_pdec_stamps = (unsigned long long*)dev; }
+void whisper_mi355x_set_pdec_blocks(int on) { wm::g_pdec_blocks = on != 0; }
 // out[M][N] (f32 for epi EPI_F32 / EPI_RESID, else the context dtype) = A[M][K] . B[N][K]^T + bias,
 // all device pointers; runs `reps` times and returns the average ms per launch in *ms.
 int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* A, int M, int K, const void* B, int N,

@@ -837,7 +837,15 @@ static int pdec_max() {
 // The per-call switches that choose a decode step's kernels, folded into the key of its captured graph.
 static int dec_path_sig() {
     return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) |
-           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26);
+           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26) | ((g_pdec_blocks & 1) << 29);
+}
+
+// Quantized files: the persistent step reads the context's expanded compute-type copy when it exists
+// (measured faster: the one-wave-per-SIMD kernel pays for the in-register dequantization; large-v3
+// q5_0, 1 clip: 2.79 ms per step streaming blocks, 1.52 reading the copy); whisper_mi355x_set_pdec_blocks(1)
+// makes it stream the GGML blocks (0.69 bytes per q5_0 weight) instead.
+static bool pdec_blocks(Context* c) {
+    return c->quant && (g_pdec_blocks || !c->expanded.load(std::memory_order_acquire));
 }
 
 // A decode step of n clips runs as one persistent launch when the model shape has a kernel, the
@@ -851,8 +859,9 @@ static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
     for (const LayerW& L : c->w.dec)
         for (const QMat* q : {&L.qqkv, &L.qo, &L.qxq, &L.qxo, &L.q1, &L.q2})
             if ((q->type != 0) != quant) return false;
-    if (quant && c->dt != DType::F16) return false;
-    if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head, quant)) return false;
+    const bool blocks = pdec_blocks(c);
+    if (blocks && c->dt != DType::F16) return false;
+    if (!pdec_supported(c->hp.n_text_state, c->hp.n_text_head, blocks)) return false;
     static const int cus = [] {
         int dev = 0, v = 0;
         hipGetDevice(&dev);
@@ -862,32 +871,36 @@ static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
     return cus == 256;
 }
 
-// Device array of the decoder layers' pointers (once per context)
-static const PdecLayer* pdec_layers(Context* c) {
+// Device array of the decoder layers' pointers (once per context and weight form): the arena's
+// matrices, the GGML blocks of a quantized file, or that file's expanded compute-type copy
+static const PdecLayer* pdec_layers(Context* c, bool blocks) {
     std::lock_guard<std::mutex> lk(c->pdec_mu);
-    if (!c->pdec_layers) {
+    void*& slot = blocks || !c->quant ? c->pdec_layers : c->pdec_layers_exp;
+    if (!slot) {
         std::vector<PdecLayer> h(c->hp.n_text_layer);
         for (int l = 0; l < c->hp.n_text_layer; l++) {
             const LayerW& L = c->w.dec[l];
-            auto mat = [](const void* w, const QMat& q) {
-                return q.type ? PdecMat{q.qs, q.qh, q.dm, q.type} : PdecMat{w, nullptr, nullptr, 0};
+            LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
+            if (c->quant && !blocks) m = c->exp_dec[l];
+            auto mat = [&](const void* w, const QMat& q) {
+                return q.type && blocks ? PdecMat{q.qs, q.qh, q.dm, q.type} : PdecMat{w, nullptr, nullptr, 0};
             };
-            h[l] = PdecLayer{mat(L.wqkv, L.qqkv), mat(L.wo, L.qo), mat(L.wxq, L.qxq), mat(L.wxo, L.qxo), mat(L.w1, L.q1),
-                             mat(L.w2, L.q2), L.bqkv, L.bo, L.bxq, L.bxo, L.b1, L.b2,
+            h[l] = PdecLayer{mat(m.wqkv, L.qqkv), mat(m.wo, L.qo), mat(m.wxq, L.qxq), mat(m.wxo, L.qxo), mat(m.w1, L.q1),
+                             mat(m.w2, L.q2), L.bqkv, L.bo, L.bxq, L.bxo, L.b1, L.b2,
                              L.ln1_w, L.ln1_b, L.lnx_w, L.lnx_b, L.ln2_w, L.ln2_b};
         }
         void* p = nullptr;
         WM_CHECK(hipMalloc(&p, h.size() * sizeof(PdecLayer)));
         WM_CHECK(hipMemcpy(p, h.data(), h.size() * sizeof(PdecLayer), hipMemcpyHostToDevice));
-        c->pdec_layers = p;
+        slot = p;
     }
-    return (const PdecLayer*)c->pdec_layers;
+    return (const PdecLayer*)slot;
 }
 
 // Everything a persistent step allocates, before a decode step is captured (no hipMalloc in a capture)
 static void pdec_prepare(Context* c, whisper_state* s) {
     Workspace& w = s->ws;
-    pdec_layers(c);
+    pdec_layers(c, pdec_blocks(c));
     if (w.pd_sync) return;
     // the hand-off block
     dalloc(w.pd_sync, pdec_granules(c->hp.n_text_state, c->hp.n_text_layer, c->hp.n_text_head).bytes);
@@ -904,9 +917,10 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab;
     const int n = v.n;
     hipStream_t st = v.st;
-    if (!w.pd_sync || !c->pdec_layers) WM_FAIL("pdec: buffers not allocated (pdec_prepare)");
+    if (!w.pd_sync) WM_FAIL("pdec: buffers not allocated (pdec_prepare)");
+    const bool blocks = pdec_blocks(c);
     PdecArgs a{};
-    a.layers = (const PdecLayer*)c->pdec_layers;
+    a.layers = pdec_layers(c, blocks);
     a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.n_audio_ctx = hp.n_audio_ctx;
     a.tok_emb = c->w.tok_emb_f32 ? (const void*)c->w.tok_emb_f32 : c->w.tok_emb;
     a.te_f32 = c->w.tok_emb_f32 != nullptr;
@@ -915,7 +929,7 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
     a.self_cache = w.self; a.cross_cache = w.cross;
     a.k_scale = c->k_scale;
-    a.quant = c->w.dec[0].qqkv.type != 0;
+    a.quant = blocks;
     a.s_cross = pdec_cross_splits(n, H, hp.n_audio_ctx);
     a.sync = w.pd_sync;
     a.gr = pdec_granules(d, L, H);

@@ -114,6 +114,7 @@ struct Context {
     // persistent decode step (kernels/pdec.hip): the decoder layers' pointers as a device array
     std::mutex pdec_mu;
     void* pdec_layers = nullptr;
+    void* pdec_layers_exp = nullptr;  // (a quantized file's expanded copy)
     // States released by whisper_free_state, kept with their workspace and captured decode graphs
     // for the next whisper_init_state: whisper.rs:83-85 creates (and drops) a state on every
     // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.

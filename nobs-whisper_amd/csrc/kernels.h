@@ -250,6 +250,8 @@ struct PdecArgs {
 extern unsigned long long* g_pdec_stamps;
 // 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
 extern long g_pdec_spin_ticks;
+// 1: quantized files' persistent steps stream the GGML blocks even when the expanded copy exists
+extern int g_pdec_blocks;
 // a kernel exists for the shape: plain weights at d 384 / 512 / 768 / 1024 / 1280, GGML blocks (f16
 // compute) at 768 / 1024 / 1280
 bool pdec_supported(int d, int H, bool quant);

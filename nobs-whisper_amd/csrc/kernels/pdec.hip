@@ -20,6 +20,7 @@ constexpr int kG = 256, kNT = 256;
 
 long g_pdec_spin_ticks = 5000000;
 unsigned long long* g_pdec_stamps = nullptr;
+int g_pdec_blocks = 0;
 
 bool pdec_supported(int d, int H, bool quant) {
     if (H * 64 != d) return false;

@@ -505,6 +505,7 @@ void free_context(Context* c) {
     if (c && c->arena8) { hipSetDevice(c->device); hipFree(c->arena8); c->arena8 = nullptr; }
     if (c && c->arena_exp) { hipSetDevice(c->device); hipFree(c->arena_exp); c->arena_exp = nullptr; }
     if (c && c->pdec_layers) { hipSetDevice(c->device); hipFree(c->pdec_layers); c->pdec_layers = nullptr; }
+    if (c && c->pdec_layers_exp) { hipSetDevice(c->device); hipFree(c->pdec_layers_exp); c->pdec_layers_exp = nullptr; }
 }
 
 }  // namespace wm

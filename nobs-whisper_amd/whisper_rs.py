@@ -172,6 +172,7 @@ def lib() -> C.CDLL:
         "whisper_mi355x_kernel_stats": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
         "whisper_mi355x_set_pdec_spin": (None, [C.c_long]),
         "whisper_mi355x_set_pdec_stamps": (None, [vp]),
+        "whisper_mi355x_set_pdec_blocks": (None, [C.c_int]),
         "whisper_mi355x_find_silence_boundaries": (C.c_int, [C.c_int, C.POINTER(vp), ip, C.c_int, C.c_int, C.c_bool,
                                                              ip, ip, C.c_int, fp, fp, C.c_int]),
         "whisper_mi355x_resample_len": (C.c_int, [C.c_int, C.c_int]),

@@ -6,8 +6,9 @@ cross K/V cache form.
     oracle on every model width the kernel is built for (d 384 / 512 / 768 / 1280; 1024 is in
     tests/test_gpu_fulldepth.py), with the reference's FullParams, prompted and auto-language cases
     (a clip with an oracle near tie <= F16_GAP nats: identical up to that step);
-  * GGML-block files (the app's catalog: small-q5_1, medium-q5_0, large-v3-q5_0; plus q4_1 / q8_0) through
-    the block-streaming kernel (f16 compute): exact against the oracle like the f16 cases;
+  * GGML-block files (the app's catalog: small-q5_1, medium-q5_0, large-v3-q5_0; plus q4_1 / q8_0), both
+    through the block-streaming kernel (f16 compute) and the default expanded copy: exact against the
+    oracle like the f16 cases;
   * a batch of 4 clips (the largest it takes) against the oracle clip by clip;
   * the give-up path: with a zero spin limit every launch gives up and the step is re-run on the
     per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit;
@@ -106,9 +107,16 @@ QUANT_CASES = [("small-4L+conf+q5_1", 1, "en", None, 0.2), ("large-v3-2L+conf+q5
                ("large-v3-turbo-2L+conf+q4_1", 1, "en", None, 0.2), ("large-v3-2L+conf+q8_0", 1, None, None, 0.2)]
 
 
+@pytest.mark.parametrize("blocks", [1, 0])
 @pytest.mark.parametrize("shape,clip,lang,prompt,t_inc", QUANT_CASES)
-def test_pdec_quant_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc):
-    test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
+def test_pdec_quant_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc, blocks):
+    """blocks 1: the persistent kernel streams the GGML blocks (dequantized in registers); 0 (the
+    default): it reads the context's expanded compute-type copy of the same weights."""
+    wrs.lib().whisper_mi355x_set_pdec_blocks(blocks)
+    try:
+        test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
+    finally:
+        wrs.lib().whisper_mi355x_set_pdec_blocks(0)
 
 
 def test_pdec_batch4_vs_oracle(wrs, monkeypatch):
