@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     float* part = (float*)(smem + LL.part);  // the cross partials a merging workgroup gathers [S][66]
     int* lflag = (int*)(smem + LL.lflag);
     uint16_t* gtab = (uint16_t*)(smem + LL.gtab);  // GELU table, |x| < 10 (1-2 clips only)
-    const bool ltab = a.M <= 2;
+    const bool ltab = MAXM == 1 || a.M <= 2;  // (the one-row build never reads the global table)
 
     const int M = a.M, L = a.L, w0 = blockIdx.x, tid = ptid(), wave = tid >> 6, lane = tid & 63;
     const PdecGranules& G = a.gr;
@@ -653,8 +653,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
     wq.load(cmat(LT[0].qkv), LT[0].bqkv, 3 * D, D, true, zp);
 
     // LayerNorm gamma / beta into lnp slots (LN1 at 0, 1; cross LN at 2, 3; LN2 at 4, 5): issued into
-    // registers two phases ahead of the LayerNorm's phase (B for the cross LN, E for LN2, G for the next
-    // layer's LN1 or the final LN), stored after the next phase's wait (C, F, H)
+    // registers ahead of the LayerNorm's phase (B for the cross LN, E for LN2, H for the next layer's LN1
+    // or the final LN), stored after the next phase's wait (C, F) or before A's wait (LN1)
     constexpr int NGL = (2 * D + kNT - 1) / kNT;
     float lv[NGL];
     auto ln_issue = [&](const float* gw, const float* gb) {
@@ -707,8 +707,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                         const int cl = wave + 4 * j;
                         xcur[j][m] = (m < M && cl < c1_n) ? xf[m * D + c1_0 + cl] : 0.0f;
                     }
-            } else if (!sweep_xf(g_x0, tag(l, 0))) {
-                return;
+            } else {
+                ln_commit(0);  // (issued after the previous H's publish; the sweep's barriers order the reads)
+                if (!sweep_xf(g_x0, tag(l, 0))) return;
             }
             stamp(l, 0, 0);
             ln_rows<T, D>(xf, M, lnp, lnp + D, xs, lred);
@@ -814,7 +815,9 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
         }
         // ---- E: cross attention over the cached K/V, split over keys; split 0 of a (row, head) merges -----------
         {
-            auto ahead = [&] {  // phase G's weights and LayerNorm parameters (after the query, as in B)
+            // phase G's weights and LayerNorm parameters: a task workgroup issues them once its output is
+            // out (issuing 4d x d of weights stalls the wave while the memory pipeline is full)
+            auto ahead = [&] {
                 ln_issue(W.ln2_w, W.ln2_b);
                 wf1.load(cmat(W.f1), W.b1, 4 * D, D, true, zp);
             };
@@ -836,15 +839,16 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                            }, err, lflag, spin))
                     return;
                 stamp(l, 4, 0);
-                ahead();
                 attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res, zp);  // (no fresh row)
                 // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
                 // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
                 unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
                 if (s > 0) {
                     if (tid < kPartG) put_g(gp0 + (long)s * kPartG, tid, tag(l, 4), __builtin_bit_cast(uint32_t, res[tid]));
+                    ahead();
                 } else {
                     if (tid < kPartG) part[tid] = res[tid];
+                    ahead();  // (lands while the other splits finish)
                     if (!sweep<16>(gp0 + kPartG, (S - 1) * kPartG, tag(l, 4), [](int i) { return (long)i; },
                                    [&](int i, uint32_t b) { part[kPartG + i] = f32_of(b); }, err, lflag, spin))
                         return;
@@ -895,8 +899,8 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             __syncthreads();
             float acc[NC4][MAXM];
             wf1.template run<MAXM>(xs, D, M, acc);
-            // GELU by ggml's f16 table: the lookups are issued, then phase H's weights, then the lookups
-            // are used (waiting for them does not wait for the weight stream issued after them)
+            // GELU by ggml's f16 table (LDS up to 2 clips, the global table past that); phase H's weights
+            // are issued after the publish
             float gx[NC4];
             uint16_t gt[NC4];
 #pragma unroll
@@ -908,18 +912,16 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     if (lane == m) gx[j] = acc[j][m] + wf1.bias[j];
                 const unsigned hb = (lane < M && cl < wf1.nc) ? __builtin_bit_cast(uint16_t, (half_t)gx[j]) : 0u;
                 const unsigned hq = hb & 0x7FFF;
-                if (ltab && hq < kPdecGeluHalf) gt[j] = gtab[hq + (hb >> 15) * kPdecGeluHalf];  // (|x| < 10)
-                else gt[j] = *gp(a.gelu_tab + hb);
+                if (ltab) {
+                    // |h| < 10 from LDS; past it the table holds h itself (tanhf rounds to 1), -0 for the
+                    // negatives (1 + tanhf = 0) and the NaNs: no global lookup, so using the result never
+                    // waits on the weight stream issued below
+                    const uint16_t tv = gtab[(hq < kPdecGeluHalf ? hq : 0u) + (hb >> 15) * kPdecGeluHalf];
+                    gt[j] = hq < kPdecGeluHalf ? tv : (uint16_t)((hq > 0x7C00u || !(hb & 0x8000u)) ? hb : 0x8000u);
+                } else {
+                    gt[j] = *gp(a.gelu_tab + hb);
+                }
             }
-            asm volatile("" ::: "memory");
-            wf2.load(cmat(W.f2), W.b2, D, 4 * D, false, zp);
-            if (l + 1 < L) {
-                wq.load(cmat(LT[l + 1].qkv), LT[l + 1].bqkv, 3 * D, D, true, zp);
-                ln_issue(LT[l + 1].ln1_w, LT[l + 1].ln1_b);
-            } else {
-                ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
-            }
-            asm volatile("" ::: "memory");
 #pragma unroll
             for (int j = 0; j < NC4; j++) {
                 const int cl = wave + 4 * j;
@@ -931,11 +933,12 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             }
             publish_pairs(g_ff, 2 * D, wf1.c0, wf1.nc, tag(l, 7));
             stamp(l, 6, 1);
+            asm volatile("" ::: "memory");
+            wf2.load(cmat(W.f2), W.b2, D, 4 * D, false, zp);
         }
         // ---- H: FC2 + residual -> the next layer's x0 ------------------------------------------------------------
         {
             if (!sweep_xs(g_ff, 2 * D, tag(l, 7))) return;
-            ln_commit(0);
             stamp(l, 7, 0);
             float acc[NC1][MAXM];
             wf2.template run<MAXM>(xs, 4 * D, M, acc);
@@ -951,10 +954,18 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                     }
                 }
             stamp(l, 7, 1);
+            asm volatile("" ::: "memory");
+            if (l + 1 < L) {  // the next layer's QKV weights and LN1 (its sweep is behind them: A needs both)
+                wq.load(cmat(LT[l + 1].qkv), LT[l + 1].bqkv, 3 * D, D, true, zp);
+                ln_issue(LT[l + 1].ln1_w, LT[l + 1].ln1_b);
+            } else {
+                ln_issue(a.lnd_w, a.lnd_b);  // the final LayerNorm (workgroup 0)
+            }
         }
     }
     // ---- final LayerNorm of every row -> the logits GEMM's input ----------------------------------------------
     if (w0 == 0) {
+        ln_commit(0);
         if (!sweep_xf(g_x0, tag(L, 0))) return;
         ln_rows<T, D>(xf, M, lnp, lnp + D, (T*)a.out_dh, lred);
     }
