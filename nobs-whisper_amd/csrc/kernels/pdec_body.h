@@ -482,6 +482,7 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
         if (c0 != r0) attn_rows<T, U>(K, c0, r1, fresh, rk, zp);
 #pragma unroll
         for (int u = 0; u < U; u++) {
+            if (c0 + NG * u >= r1) break;  // (uniform: a register row of no key is not computed)
             const int t = c0 + grp + NG * u;
             const T* ke = (const T*)&rk[u];
             const bool fr = t == fresh;
@@ -518,6 +519,7 @@ __device__ __forceinline__ void attn_task(const float* qs, const T* __restrict__
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
+            if (c0 + NG * u >= r1) break;
             const int t = c0 + grp + NG * u;
             if (t < r1) {  // (rows past the range: their V registers are zero, skipped all the same)
                 const bool fr = t == fresh;
@@ -751,7 +753,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 u32x4 rk[16], rv[16];
                 attn_load<T, 16>(Kc, Vc, 0, nkv, pos, rk, rv, zp);  // the cached rows land while the query is awaited
                 // q, k, v of head h: granules h * 32 + i of each third of the row
-                if (!sweep(g_qkv, 96, tag(l, 1), [&](int i) { return (long)m * (3 * D / 2) + (i >> 5) * (D / 2) + h * 32 + (i & 31); },
+                if (!sweep<1>(g_qkv, 96, tag(l, 1), [&](int i) { return (long)m * (3 * D / 2) + (i >> 5) * (D / 2) + h * 32 + (i & 31); },
                            [&](int i, uint32_t b) {
                                qf[2 * i] = (float)lo_t<T>(b);
                                qf[2 * i + 1] = (float)hi_t<T>(b);
@@ -832,7 +834,7 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                 const T* Vc = cross + (((sl * L + l) * 2 + 1) * H + h) * (long)T_ * 64;
                 u32x4 rk[8], rv[8];
                 attn_load<T, 8>(Kc, Vc, r0, r1, -1, rk, rv, zp);  // constant for the window: issued before the wait
-                if (!sweep(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
+                if (!sweep<1>(g_qx, 32, tag(l, 4), [&](int i) { return (long)m * (D / 2) + h * 32 + i; },
                            [&](int i, uint32_t b) {
                                qf[2 * i] = (float)lo_t<T>(b);
                                qf[2 * i + 1] = (float)hi_t<T>(b);
