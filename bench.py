@@ -173,11 +173,12 @@ def cross_step_grid(direct: bool, nb: int, heads: int, wide_max: int = 4) -> int
     return nb * heads * (1024 if nb <= wide_max else 256)
 
 
-def pmc_traffic(kernel_class: str, direct: bool | None, grid_threads: int | None):
+def pmc_traffic(kernel_class: str, direct: bool | None, grid_threads: int | None, sym_re: str = ""):
     """Launch-weighted HBM bytes per launch (FETCH_SIZE doubled per the gfx950 correction, +
     WRITE_SIZE) of the kernel this class launched in the timed steps, from profiles/PMC_TRAFFIC_FILE:
-    matched by kernel symbol (and cross form) AND grid size, or None when that pass did not profile
-    this exact launch shape."""
+    matched by kernel symbol (and cross form) AND grid size (and sym_re: the persistent step's width and
+    compute type, whose grid is the same for every model), or None when that pass did not profile this
+    exact launch shape."""
     import re
     pat = K_SYMBOL.get((kernel_class, direct if kernel_class == "attn_cross_decode" else None))
     path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
@@ -188,7 +189,7 @@ def pmc_traffic(kernel_class: str, direct: bool | None, grid_threads: int | None
     n = tb = 0.0
     for sym, v in data.items():
         name, _, grid = sym.partition("@grid=")
-        if re.search(pat, name) and grid == str(grid_threads):
+        if re.search(pat, name) and grid == str(grid_threads) and re.search(sym_re, name):
             n += v["launches"]
             tb += v["traffic_bytes"] * v["launches"]
     return (tb / n if n else None), PMC_TRAFFIC_FILE
@@ -662,9 +663,13 @@ def main():
         if K_NAMES[dom] == "attn_cross_decode":
             from make_model import SHAPES
             grid = cross_step_grid(bool(form["direct"]), nb, SHAPES[args.model][3])
-        elif K_NAMES[dom] == "pdec_step":
+        sym_re = ""
+        if K_NAMES[dom] == "pdec_step":
+            from make_model import SHAPES
             grid = 256 * 256  # one 256-thread workgroup per CU, whatever the clip count
-        traffic, src = pmc_traffic(K_NAMES[dom], form["direct"], grid)
+            # pdec_kernel<T, D, ...>: mangled T is DF16_ (f16) or DF16b (bf16), then Li<D>E
+            sym_re = r"pdec_kernelI%s_?Li%dE" % ("DF16" if args.dtype == "f16" else "DF16b", SHAPES[args.model][2])
+        traffic, src = pmc_traffic(K_NAMES[dom], form["direct"], grid, sym_re)
         if traffic is not None:
             roof.update(traffic=round(traffic / 1e6, 3), traffic_unit="MB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                         traffic_source=f"profiles/{src}")
