@@ -46,7 +46,10 @@ PdecGranules pdec_granules(int d, int L, int H) {
     return g;
 }
 
-int pdec_cross_splits(int M, int H, int rows) { return std::max(1, std::min(kG / (M * H), rows / 16)); }
+// at most 8 key splits per (row, head): the split-0 merge reads fewer partials and fewer workgroups poll
+// (measured at 1 clip, caps 6 / 8 / 16 / none: base 191.5 / 188.5 / 192.0 / 195.8 us per step, large-v3
+// unchanged within noise)
+int pdec_cross_splits(int M, int H, int rows) { return std::max(1, std::min({kG / (M * H), rows / 16, 8})); }
 
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
     if (a.M < 1 || a.M > kPdecMaxRows) WM_FAIL("pdec: %d rows", a.M);
