@@ -332,7 +332,9 @@ def app_pattern(wrs, model_dir: str, shape: str, dtype: str, calls: int) -> dict
     filtered. Latency per call = host wall clock around transcribe (PCM on the host, results on the
     host). Measured with the context's state pool (default: a released state keeps its workspace and
     decode graphs for the next call) and without it (WHISPER_MI355X_STATE_POOL=0: every call allocates
-    its workspace and captures its decode graphs, as a plain whisper.cpp state would)."""
+    its workspace and captures its decode graphs, as a plain whisper.cpp state would). Every call's decoded
+    tokens (all decode steps of all attempts, whisper_mi355x_decoded_tokens_total around the call) are
+    reported beside its latency, so calls that decode more tokens are not mistaken for slower ones."""
     import numpy as np
     from make_model import synthetic_pcm
     path = os.path.join(model_dir, f"{shape}_s0.bin")
@@ -344,19 +346,25 @@ def app_pattern(wrs, model_dir: str, shape: str, dtype: str, calls: int) -> dict
         os.environ["WHISPER_MI355X_STATE_POOL"] = pool
         eng = wrs.WhisperEngine()
         assert eng.load_model(path) == 0
-        last, lat, chars = None, [], 0
+        last, lat, toks, chars = None, [], [], 0
+        L = wrs.lib()
         for x in chunks:
+            k0 = L.whisper_mi355x_decoded_tokens_total()
             t = time.perf_counter()
             rc, text = eng.transcribe(x, None, wrs.DEFAULT_VOCABULARY, last)
             lat.append(time.perf_counter() - t)
+            toks.append(L.whisper_mi355x_decoded_tokens_total() - k0)
             assert rc == 0, rc
             last = text or None
             chars += len(text or "")
         del eng
         steady = sorted(lat[1:]) or lat
+        per_tok = sorted(1e3 * a / max(1, b) for a, b in list(zip(lat, toks))[1:]) or [1e3 * lat[0] / max(1, toks[0])]
         out[label] = dict(first_call_ms=round(lat[0] * 1e3, 1), median_ms=round(1e3 * steady[len(steady) // 2], 1),
                           min_ms=round(1e3 * min(steady), 1),
-                          rtf_inverse_median=round(25.2 / steady[len(steady) // 2], 1))
+                          rtf_inverse_median=round(25.2 / steady[len(steady) // 2], 1),
+                          decoded_tokens_per_call=toks, ms_per_decoded_token_median=round(per_tok[len(per_tok) // 2], 3),
+                          ms_per_call=[round(1e3 * a, 1) for a in lat])
     out["text_chars_total"] = chars
     os.environ.pop("WHISPER_MI355X_STATE_POOL", None)
     os.environ.pop("WHISPER_MI355X_DTYPE", None)
@@ -703,8 +711,8 @@ def main():
             app = []
             try:
                 app.append(app_pattern(wrs, args.model_dir, "base+conf", "f16", args.app_calls))
-                app.append(app_pattern(wrs, args.model_dir, shape, "bf16" if args.dtype != "f16" else "f16",
-                                       args.app_calls))
+                # f16: the engine's default compute type (capi.cpp whisper_init_*: the GGML file's own type)
+                app.append(app_pattern(wrs, args.model_dir, shape, "f16", args.app_calls))
             except Exception as e:  # reported, never fatal to the GPU number
                 app.append(dict(error=str(e)))
         cpu = None
@@ -739,6 +747,7 @@ def main():
                       "phase_ms_last_step": {k: round(v, 1) for k, v in phases.items()},
                       "warmup_step_s": round(warm_s, 3), "model_load_s": round(load_s, 2),
                       "weight_broadcast_s": round(bcast_s, 3), "frontend": frontend,
+                      "pdec_give_ups": L.whisper_mi355x_pdec_give_ups(None),
                       "weight_arena_bytes": arena_bytes},
         }
         print(json.dumps(line), flush=True)

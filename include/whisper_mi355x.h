@@ -52,7 +52,8 @@ WHISPER_API int whisper_mi355x_full_batch(struct whisper_context * ctx, struct w
  * is forced[j * fixed_tokens + i] (whatever the logits rules chose), and the raw logits of the jobs
  * spot[0..n_spot) at every step i (step 0 = the prefill) go to spot_logits[(i * n_spot + k) * n_vocab]
  * (host memory, fixed_tokens * n_spot * n_vocab floats). The kernels are the ones whisper_mi355x_full_batch
- * runs on the same batch. n_jobs <= 128. */
+ * runs on the same batch (above 128 jobs: two concurrent halves, each forced and spot-copied by its own
+ * jobs). */
 WHISPER_API int whisper_mi355x_full_batch_forced(struct whisper_context * ctx, struct whisper_state * state,
                                                  struct whisper_full_params params, const float * const * pcm,
                                                  const int * n_samples, int n_jobs, bool pcm_on_device, int fixed_tokens,
@@ -66,6 +67,9 @@ WHISPER_API whisper_token_data whisper_mi355x_batch_token_data(struct whisper_st
 WHISPER_API int whisper_mi355x_batch_lang_id(struct whisper_state * state, int job);
 /* tokens generated (all decode steps, all attempts) by the last whisper_mi355x_full_batch */
 WHISPER_API long whisper_mi355x_batch_decoded_tokens(struct whisper_state * state);
+/* tokens generated by every whisper_full / whisper_mi355x_full_batch call of the process so far (lets a
+ * caller that drives whisper.h through its own states, e.g. the WhisperEngine mirror, count per call) */
+WHISPER_API long whisper_mi355x_decoded_tokens_total(void);
 
 /* Per-window decisions of whisper_full's temperature-fallback loop (the integer outcomes that are
  * comparable with whisper.cpp even when a sampled t > 0 attempt is not): one record per decoded
@@ -108,6 +112,14 @@ WHISPER_API int whisper_mi355x_get_encoder_out(struct whisper_state * state, flo
  * Every call resets the counters; stats out = {total ms, launches, total work}. */
 WHISPER_API int whisper_mi355x_kernel_timing(struct whisper_state * state, int class_mask);
 WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cls, double out[3]);
+/* Pseudo class of whisper_mi355x_kernel_stats: out = {ms lost, give-ups, 0} of the persistent decode step
+ * (kernels/pdec.hip) on this state since it was created (or recycled): a launch that gave up (not all of its
+ * 256 workgroups became resident within the wait limit, e.g. another process held CUs) is re-run on the
+ * per-kernel path, and the state's next steps take that path for about a second. Not reset by
+ * whisper_mi355x_kernel_timing. whisper_mi355x_pdec_give_ups returns the count alone (NULL: the total of every
+ * state of the process). */
+#define WHISPER_MI355X_KSTAT_PDEC_GIVE_UPS 100
+WHISPER_API long whisper_mi355x_pdec_give_ups(struct whisper_state * state);
 
 /* Kernel-level test/tuning hooks (device pointers): one fused-epilogue GEMM launch of the engine
  * (epi as in kernels.h: 0 store, 1 gelu, 2 residual f32, 4 f32), averaged over reps; and the
@@ -124,8 +136,9 @@ WHISPER_API int whisper_mi355x_debug_gemm_small(struct whisper_context * ctx, in
                                                 const float * ln_w, const float * ln_b, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
 /* Test hook: a persistent decode step's waits give up after this many 100 MHz ticks (default 5,000,000 =
- * 50 ms); 0 makes every persistent launch give up, so each step takes the re-run path. Captured graphs
- * keep the value they were captured with. */
+ * 50 ms); 0 makes every persistent launch give up, so each step takes the re-run path. Decode graphs
+ * captured before the call are retired (not replayed) once it changes the value; likewise for the stamps
+ * pointer below, so a freed stamps buffer is never written. */
 WHISPER_API void whisper_mi355x_set_pdec_spin(long ticks);
 /* Profiling hook: device buffer of 256 * n_text_layer * 8 * 2 u64 that persistent decode steps captured
  * from now on fill with the 100 MHz clock (per workgroup, layer and phase: input arrived, phase

@@ -543,6 +543,12 @@ int whisper_mi355x_kernel_timing(struct whisper_state* s, int class_mask) {
     return 0;
 }
 int whisper_mi355x_kernel_stats(struct whisper_state* s, int cls, double out[3]) {
+    if (s && cls == WHISPER_MI355X_KSTAT_PDEC_GIVE_UPS) {
+        out[0] = s->pdec_lost_ms;
+        out[1] = (double)s->pdec_give_ups;
+        out[2] = 0.0;
+        return 0;
+    }
     if (!s || cls < 0 || cls >= K_NCLASS) return -1;
     out[0] = s->kstat[cls].ms;
     out[1] = (double)s->kstat[cls].count;
@@ -553,8 +559,16 @@ int whisper_mi355x_kernel_stats(struct whisper_state* s, int cls, double out[3])
 
 void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
 void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
-void whisper_mi355x_set_pdec_spin(long ticks) { wm::g_pdec_spin_ticks = ticks; }
-void whisper_mi355x_set_pdec_stamps(void* dev) { wm::g_pdec_stamps = (unsigned long long*)dev; }
+void whisper_mi355x_set_pdec_spin(long ticks) {
+    wm::g_pdec_spin_ticks = ticks;
+    wm::g_pdec_gen++;
+}
+void whisper_mi355x_set_pdec_stamps(void* dev) {
+    wm::g_pdec_stamps = (unsigned long long*)dev;
+    wm::g_pdec_gen++;
+}
+long whisper_mi355x_decoded_tokens_total(void) { return wm::g_decoded_tokens_total.load(); }
+long whisper_mi355x_pdec_give_ups(struct whisper_state* s) { return s ? s->pdec_give_ups : wm::g_pdec_give_ups_total.load(); }
 void whisper_mi355x_set_pdec_blocks(int on) { wm::g_pdec_blocks = on != 0; }
 // out[M][N] (f32 for epi EPI_F32 / EPI_RESID, else the context dtype) = A[M][K] . B[N][K]^T + bias,
 // all device pointers; runs `reps` times and returns the average ms per launch in *ms.

@@ -180,6 +180,10 @@ static void reset_for_reuse(whisper_state* s) {
     s->ktime_mask = 0;
     for (auto& k : s->kstat) k = KStat();
     s->cur_self_work = 0;
+    s->pdec_give_ups = 0;
+    s->pdec_lost_ms = 0;
+    s->pdec_off_until = 0;
+    s->pdec_off = false;
     std::fill(s->ws.cross_fresh.begin(), s->ws.cross_fresh.end(), 0);
 }
 
@@ -852,7 +856,7 @@ static bool pdec_blocks(Context* c) {
 // weights are f16 / bf16 or GGML blocks (not the fp8 decoder copies), the device has the 256 CUs the
 // grid is built for, and the step is in the cross K/V cache form.
 static bool pdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
-    if (xdirect || s->pdec_block || n < 1 || n > pdec_max()) return false;
+    if (xdirect || s->pdec_block || s->pdec_off || n < 1 || n > pdec_max()) return false;
     if (c->fp8_enc && !c->dec8.empty()) return false;
     // one weight form for every decoder matrix (the kernel is built per form)
     const bool quant = c->w.dec[0].qqkv.type != 0;
@@ -930,7 +934,7 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     a.self_cache = w.self; a.cross_cache = w.cross;
     a.k_scale = c->k_scale;
     a.quant = blocks;
-    a.s_cross = pdec_cross_splits(n, H, hp.n_audio_ctx);
+    a.s_cross = pdec_cross_splits(H, hp.n_audio_ctx);
     a.sync = w.pd_sync;
     a.gr = pdec_granules(d, L, H);
     a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
@@ -1604,6 +1608,10 @@ static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, st
 
 // One decode step (decoder over n active clips + logits kernel) as a replayed hipGraph: the host
 // cost of ~11 launches per layer is paid once per distinct n at capture time.
+// After a persistent launch gave up, the state's steps take the per-kernel path for this long (a co-tenant
+// holding CUs would otherwise cost the 50 ms timeout on every step)
+static const double kPdecBackoffMs = 1000.0;
+
 static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::vector<float>>& probs_rows) {
     Context* c = S.c;
     whisper_state* s = S.s;
@@ -1612,13 +1620,26 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     const bool any = logits_prepare(S, act, false);
     whisper_state::DecGraph* G = nullptr;
     const int sig = dec_path_sig();
+    const double t_step = now_ms();
+    s->pdec_off = s->pdec_give_ups > 0 && t_step < s->pdec_off_until;
     const bool pd = pdec_use(c, s, n, s->direct);
     if (pd) pdec_prepare(c, s);
+    // retire persistent-step graphs captured under an older stamps pointer / spin limit (g_pdec_gen)
+    for (size_t i = 0; i < s->dec_graphs.size();) {
+        auto& g = s->dec_graphs[i];
+        if (g.pdec && g.gen != g_pdec_gen) {
+            hipGraphExecDestroy(g.exec);
+            for (auto& e : g.ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+            s->dec_graphs.erase(s->dec_graphs.begin() + i);
+        } else {
+            i++;
+        }
+    }
     for (auto& g : s->dec_graphs)
         if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd)
             G = &g;
     if (!G) {
-        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, nullptr, {}};
+        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, g_pdec_gen, nullptr, {}};
         hipGraph_t graph;
         s->capture_ev = &g.ev;
         WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
@@ -1638,11 +1659,12 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         return;
     }
     // A persistent launch needs its 256 workgroups resident together: persistent steps of different
-    // states (threads) of this process never overlap, so two of them cannot hold half the CUs each.
-    static std::mutex pdec_run_mu;
+    // states (threads) of this process on one device never overlap, so two of them cannot hold half the
+    // CUs each (steps on different devices do not wait for each other)
+    static std::mutex pdec_run_mu[16];
     bool gave_up;
     {
-        std::lock_guard<std::mutex> lk(pdec_run_mu);
+        std::lock_guard<std::mutex> lk(pdec_run_mu[c->device & 15]);
         WM_CHECK(hipGraphLaunch(G->exec, s->stream));
         logits_finish(S, n, any, probs_rows);
         gave_up = *s->ws.h_pd_err != 0;
@@ -1651,7 +1673,8 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     if (!gave_up) return;
     // the launch gave up (a wait timed out: not every workgroup became resident): the step again on
     // the per-kernel path, which rewrites everything the launch may have written (the self K/V rows of
-    // this position)
+    // this position); counted (whisper_mi355x_pdec_give_ups) and followed by kPdecBackoffMs of steps on
+    // the per-kernel path
     static bool warned = false;
     if (!warned) fprintf(stderr, "whisper_mi355x: persistent decode step timed out; step re-run on the per-kernel path\n");
     warned = true;
@@ -1666,6 +1689,10 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         throw;
     }
     s->pdec_block = false;
+    s->pdec_give_ups++;
+    g_pdec_give_ups_total++;
+    s->pdec_off_until = now_ms() + kPdecBackoffMs;
+    s->pdec_lost_ms += now_ms() - t_step;
 }
 
 // Batches above kPairMin clips run as two independent halves at
@@ -1676,6 +1703,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
 // in flight measured 3720 vs 3201 audio-s/s back to back (profiles/r03_overlap_two_batches.txt),
 // where one 256-row decode step ran as two lockstep row groups before.
 static const int kPairMin = 128;
+std::atomic<long> g_decoded_tokens_total{0};
 
 static int full_batch_one(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                           int n_jobs, bool on_device, const FullOpts& o, bool single_api);
@@ -1701,15 +1729,28 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
         };
         pp.abort_callback_user_data = &gate;
     }
+    // teacher forcing (a parity-test hook) by halves: each half sees its own jobs' forced rows, and the spot
+    // jobs of the other half never match (-1); both write their own rows of the caller's spot_logits
+    FullOpts oa = o, ob = o;
+    std::vector<int> spot_a, spot_b;
+    if (o.n_spot > 0 && o.spot) {
+        for (int k = 0; k < o.n_spot; k++) {
+            spot_a.push_back(o.spot[k] < na ? o.spot[k] : -1);
+            spot_b.push_back(o.spot[k] >= na ? o.spot[k] - na : -1);
+        }
+        oa.spot = spot_a.data();
+        ob.spot = spot_b.data();
+    }
+    if (o.forced) ob.forced = o.forced + (long)na * o.fixed_tokens;
     std::thread th([&] {
         try {
-            rb = full_batch_one(c, t, pp, pcm + na, n + na, n_jobs - na, on_device, o, false);
+            rb = full_batch_one(c, t, pp, pcm + na, n + na, n_jobs - na, on_device, ob, false);
         } catch (...) {
             eb = std::current_exception();
         }
     });
     try {
-        ra = full_batch_one(c, s, pp, pcm, n, na, on_device, o, false);
+        ra = full_batch_one(c, s, pp, pcm, n, na, on_device, oa, false);
     } catch (...) {
         ea = std::current_exception();
     }
@@ -1725,6 +1766,10 @@ int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const
         s->decisions.push_back(std::move(t->decisions[j]));
     }
     s->decoded_tokens += t->decoded_tokens;
+    s->pdec_give_ups += t->pdec_give_ups;
+    s->pdec_lost_ms += t->pdec_lost_ms;
+    t->pdec_give_ups = 0;
+    t->pdec_lost_ms = 0;
     // the halves ran concurrently: a phase lasted as long as its slower half; kernel time adds up
     for (int k = 0; k < 5; k++) s->phase_ms[k] = std::max(s->phase_ms[k], t->phase_ms[k]);
     for (int k = 0; k < K_NCLASS; k++) {
@@ -1976,6 +2021,7 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
     }
     kt_flush(s);
     s->decoded_tokens = S.decoded;
+    g_decoded_tokens_total += S.decoded;
     s->phase_ms[0] = S.t_mel; s->phase_ms[1] = S.t_enc; s->phase_ms[2] = S.t_prefill; s->phase_ms[3] = S.t_decode;
     s->phase_ms[4] = S.t_logits;
     std::lock_guard<std::mutex> lk(c->timings_mu);

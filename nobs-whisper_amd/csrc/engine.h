@@ -231,12 +231,21 @@ struct whisper_state {
     // decode steps replayed as hipGraphs, one per (active-clip count, timing mask, cross form, path
     // signature): `sig` encodes the per-call switches that pick the step's kernels (dec_path_sig), so a
     // changed setting never replays a graph captured for another path
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; bool pdec; hipGraphExec_t exec; std::vector<KPending> ev; };
+    // (gen: g_pdec_gen when a persistent step was captured; its graph holds the stamps pointer and spin limit of
+    // that time, so a setter call retires it)
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; bool pdec; int gen; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step
     whisper_state* twin = nullptr;                // second half of a paired batch (full_batch)
     bool pdec_block = false;                      // re-running a step whose persistent launch gave up
+    // persistent launches of this state that gave up (a wait timed out: not all 256 workgroups resident, e.g.
+    // beside another process's kernels) and were re-run on the per-kernel path; after one, the state's steps
+    // take the per-kernel path for kPdecBackoffMs (pdec_off) instead of paying the timeout on every step
+    long pdec_give_ups = 0;
+    double pdec_lost_ms = 0;    // wall time of the given-up launches (wait until give-up + the re-run)
+    double pdec_off_until = 0;  // now_ms() clock
+    bool pdec_off = false;
 };
 
 struct whisper_context {
@@ -268,6 +277,8 @@ struct FullOpts {
 };
 // whisper_full over n_jobs clips. B=1 with the state's own prompt_past/rng reproduces
 // whisper_full_with_state; B>1 treats every clip as a fresh state.
+// tokens decoded by every whisper_full / full_batch call of the process (whisper_mi355x_decoded_tokens_total)
+extern std::atomic<long> g_decoded_tokens_total;
 int full_batch(Context* c, whisper_state* s, const whisper_full_params& p, const float* const* pcm, const int* n,
                int n_jobs, bool on_device, const FullOpts& o, bool single_api);
 

@@ -1,6 +1,8 @@
 // Host-side launchers of the gfx950 kernels. Every launcher takes the stream it runs on and
 // never allocates or synchronises (so a decode step can be captured into a hipGraph).
 #pragma once
+#include <atomic>
+
 #include "common.h"
 
 namespace wm {
@@ -194,8 +196,8 @@ struct PdecLayer {
 // The hand-off block (one allocation, zeroed before every launch): data-tagged 8-byte granules (offsets
 // in granules): x rows x0, x1, x2 [R][d] (f32), and packed T pairs: qkv [R][3d/2], self-attention output
 // so [R][d/2], cross q qx [R][d/2], cross-attention output xo [R][d/2], GELU rows ff [R][2d]; the
-// cross-attention split partials part [256][66] (f32: o[64], max, sum); then the error word (byte
-// offset); R = kPdecMaxRows.
+// cross-attention split partials part [max(256, R * H * S)][66] (f32: o[64], max, sum; one per task); then the
+// error word (byte offset); R = kPdecMaxRows.
 struct PdecGranules {
     long x0, x1, x2, qkv, so, qx, xo, ff, part;
     long err_bytes, zero_bytes, bytes;  // the error word; 256 zero bytes that no one writes (a zero page)
@@ -222,7 +224,7 @@ __host__ __device__ inline PdecLds pdec_lds(int d, int M, int S) {
     l.qf = o; o += 192 * 4;
     l.res = o; o += up(68 * 4);
     l.ost = o; o += up(l.rows * l.cmax * 4);
-    l.lred = o; o += 8 * 8;
+    l.lred = o; o += 2 * kPdecMaxRows * 4 * 8;
     l.lnp = o; o += up(6 * d * 4);
     l.part = o; o += up(S * 66 * 4);
     l.lflag = o; o += 16;
@@ -248,6 +250,11 @@ struct PdecArgs {
     unsigned long long* stamps;         // debug (g_pdec_stamps): [256][L][8][2] clock at input / publish, or null
 };
 extern unsigned long long* g_pdec_stamps;
+// bumped by the stamps / spin setters: decode graphs captured with a persistent step under an older value
+// are retired, not replayed (they hold the old pointer and limit as kernel arguments)
+extern int g_pdec_gen;
+// persistent launches that gave up, every state of the process (whisper_mi355x_pdec_give_ups(NULL))
+extern std::atomic<long> g_pdec_give_ups_total;
 // 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
 extern long g_pdec_spin_ticks;
 // 1: quantized files' persistent steps stream the GGML blocks even when the expanded copy exists
@@ -255,7 +262,7 @@ extern int g_pdec_blocks;
 // a kernel exists for the shape: plain weights at d 384 / 512 / 768 / 1024 / 1280, GGML blocks (f16
 // compute) at 768 / 1024 / 1280
 bool pdec_supported(int d, int H, bool quant);
-int pdec_cross_splits(int M, int H, int rows);
+int pdec_cross_splits(int H, int rows);  // key splits per (clip, head): a function of the shape only
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st);
 const uint16_t* gelu_table_device();
 

@@ -21,6 +21,8 @@ constexpr int kG = 256, kNT = 256;
 long g_pdec_spin_ticks = 5000000;
 unsigned long long* g_pdec_stamps = nullptr;
 int g_pdec_blocks = 0;
+int g_pdec_gen = 0;
+std::atomic<long> g_pdec_give_ups_total{0};
 
 bool pdec_supported(int d, int H, bool quant) {
     if (H * 64 != d) return false;
@@ -39,7 +41,7 @@ PdecGranules pdec_granules(int d, int L, int H) {
     g.qx = o; o += R * d / 2;
     g.xo = o; o += R * d / 2;
     g.ff = o; o += R * 2 * d;
-    g.part = o; o += (long)kG * 66;
+    g.part = o; o += (long)std::max(kG, (int)R * H * pdec_cross_splits(H, 1 << 20)) * 66;  // every task's partial
     g.err_bytes = o * 8;
     g.zero_bytes = g.err_bytes + 16;
     g.bytes = g.zero_bytes + 256;
@@ -48,12 +50,14 @@ PdecGranules pdec_granules(int d, int L, int H) {
 
 // at most 8 key splits per (row, head): the split-0 merge reads fewer partials and fewer workgroups poll
 // (measured at 1 clip, caps 6 / 8 / 16 / none: base 191.5 / 188.5 / 192.0 / 195.8 us per step, large-v3
-// unchanged within noise)
-int pdec_cross_splits(int M, int H, int rows) { return std::max(1, std::min({kG / (M * H), rows / 16, 8})); }
+// unchanged within noise). A function of the model shape only, not of the clip count (round 5, ADVICE r4:
+// a clip's result must not change with the number of clips still decoding): above 256 tasks (large-v3 at
+// 2-4 clips) workgroups take several.
+int pdec_cross_splits(int H, int rows) { return std::max(1, std::min({kG / H, rows / 16, 8})); }
 
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st) {
     if (a.M < 1 || a.M > kPdecMaxRows) WM_FAIL("pdec: %d rows", a.M);
-    if (a.M * (a.d / 64) * a.s_cross > kG) WM_FAIL("pdec: split count");
+    if ((long)a.M * (a.d / 64) * a.s_cross * 66 > a.gr.err_bytes / 8 - a.gr.part) WM_FAIL("pdec: split count");
     // self attention in one chunk (16 rows per lane group); cross-attention tasks of at most 1536 rows (the
     // scores buffer)
     if (a.n_text_ctx > 16 * kNT / 8 || (a.n_audio_ctx + a.s_cross - 1) / a.s_cross > 1536) WM_FAIL("pdec: context sizes");

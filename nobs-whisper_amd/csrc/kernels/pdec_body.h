@@ -1,39 +1,44 @@
-// Persistent decode step for few clips (the kernel; instantiated by pdec_f16.hip, pdec_bf16.hip, pdec_q.hip): the whole decoder (every layer) of one decode step in ONE
-// launch, its phases handing off through the L2 with counters instead of kernel boundaries
-// (the hot loop of whisper_full: whisper.rs:127-129 -> state.rs:147; the app
-// transcribes one clip per call, so this is the latency its user feels).
+// Persistent decode step for few clips (the kernel; instantiated by pdec_f16.hip, pdec_bf16.hip, pdec_q.hip and
+// their one-row *_1.hip builds): the whole decoder (every layer) of one decode step of <= kPdecMaxRows clips in
+// ONE launch, its phases handing off through data-tagged granules instead of kernel boundaries (SURVEY.md §8a
+// row a10, the hot loop of whisper_full: whisper.rs:127-129 -> state.rs:147; the app transcribes one clip per
+// call, so this is the latency its user feels).
 //
 // Why: at one clip a large-v3 decoder layer streams 46 MB of weights +
 // 7.7 MB of cross K/V (~8 us at HBM speed) but took ~78 us as 8 dependent launches of 5-15 us each:
 // launch boundaries, ramp-up and dependent-load latency, not bytes. Here the grid is one 256-thread
 // workgroup per CU (G = 256), resident for the whole step:
 //   per layer, 8 phases:  A  LN1 + QKV projection (+ q/k scale, rounding to T)        all WGs, column slices
-//                         B  self attention over the cache, split over keys            (clip, head, split) tasks
-//                         C  split merge + out projection + residual                   all WGs
+//                         B  self attention over the cache + this position             one (clip, head) task per WG
+//                         C  out projection + residual                                 all WGs
 //                         D  LN + cross-Q projection (+ scale)                         all WGs
-//                         E  cross attention over the cached K/V, split over keys      (clip, head, split) tasks
-//                         F  split merge + cross-out projection + residual             all WGs
+//                         E  cross attention over the cached K/V, split over keys;     (clip, head, split) tasks,
+//                            split 0 of each (clip, head) merges the splits             dealt round-robin
+//                         F  cross-out projection + residual                           all WGs
 //                         G  LN + FC1 + GELU (ggml's f16 table)                       all WGs
 //                         H  FC2 + residual                                            all WGs
 //   then the final LayerNorm of every row (the logits GEMM is the next launch).
 // A projection phase: each WG owns a contiguous slice of output columns (N / G of them), so its weights
-// are ONE contiguous range of the [N][K] matrix; it issues their loads into registers BEFORE waiting for
-// the phase's input, so the weight stream of phase p overlaps the hand-off of phase p-1 (the loader-runs-
-// ahead idea of MI355X_MICROARCH.md "prefetch-credit", in registers instead of an LDS ring). Every WG
-// gathers the whole (small) input vector: M rows of d, computes the LayerNorm itself (ggml_norm: double
-// sums) and stages the rows in LDS as T; one wave per output column, lanes split K, f32 accumulation.
+// are ONE contiguous range of the [N][K] matrix; it issues their loads into registers a phase ahead, after
+// its previous publish (the loader-runs-ahead idea of MI355X_MICROARCH.md "prefetch-credit", in registers
+// instead of an LDS ring). Every WG gathers the whole (small) input: M rows of d, computes the LayerNorm
+// itself (ggml_norm: double sums in one canonical order for every M) and stages the rows in LDS as T; one
+// wave per output column, lanes split K, f32 accumulation, wave sums by DPP.
 //
-// Hand-offs (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility", Valid forms, table
-// row 1): every payload word is stored write-through (sc1) and drained (s_waitcnt vmcnt(0) in every
-// storing wave), the workgroup barrier, then ONE lane adds 1 to the phase's counter (agent-scope atomic),
-// sharded per XCD (8 words, blockIdx % 8) so 256 arrivals spread over 8 lines; the consumer's wave 0
-// polls the 8 shards with sc1 loads (+ s_sleep) until all G workgroups arrived, the workgroup barrier,
-// then EVERY load of a handed-off byte is an sc1 load (no acquire fence needed: the row's conditions
-// hold). Counters are per (layer, phase), zeroed by a memset node before every launch.
-// Bounded spins: a wait gives up after ~50 ms (s_memrealtime, 100 MHz), sets the error word and the
-// workgroup exits; every other wait sees the error word and exits too, so the grid always drains (e.g.
-// when another kernel holds CUs and not all 256 workgroups can be resident). The host then re-runs the
-// step on the launch-per-kernel path (engine.cpp), so a failed launch costs time, never results.
+// Hand-offs (cdna_hip_programming.md Guideline 16 R2; MI355X_MICROARCH.md rows handoff-1to1 / allgather):
+// every handed-off value travels as ONE naturally aligned 8-byte granule {tag, 32 data bits} written by one
+// sc1 store; the data is the flag. A producer neither drains nor signals; a consumer re-reads the granules it
+// needs with sc1 loads (16 in flight per thread in the wide sweeps) until every tag equals the phase's tag
+// (layer * 8 + phase + 1), then uses the data bits. x rows travel as f32 granules, everything rounded to T
+// (q/k/v, attention outputs, cross-Q, GELU rows) as packed T pairs; a cross-attention split publishes its
+// partial {o[64], max, sum} as 66 granules that split 0's workgroup gathers. The block is zeroed by a memset
+// node before every launch, and a buffer is reused by the next layer (safe: every layer's phase A reads all
+// of x0, i.e. waits for every workgroup's last phase of the layer before).
+// Bounded waits: a wait gives up after spin_ticks of s_memrealtime (100 MHz; 50 ms by default), sets the
+// error word and the workgroup exits; every other wait sees the error word and exits too, so the grid always
+// drains (e.g. when another kernel holds CUs and not all 256 workgroups can be resident). The host then
+// re-runs the step on the launch-per-kernel path (engine.cpp decode_step; counted as a give-up in the
+// state's kernel stats), so a failed launch costs time, never results.
 //
 // Numerics (vs oracle/oracle_whisper.cpp, ggml's): LayerNorm as layernorm_kernel (double sums, separately
 // rounded ops, output rounded to T = ggml's f16 src1); projections f32-accumulated products of T
@@ -41,8 +46,10 @@
 // attention scores f32, softmax in f32 over each split with the split's own max, the unnormalised
 // weights rounded to T before P.V (ggml rounds the normalised P to f16: another rounding point, the
 // same precision), splits merged with exp(m_s - m) in f32 and the result rounded to T (the out
-// projection's src1). Results per row do not depend on the other rows' presence for a fixed (M, H):
-// the split count is a function of M (batch == single holds within the path at equal M only).
+// projection's src1). A row's results do not depend on the other rows (round 5): the key-split count is a
+// function of the model shape (pdec_cross_splits), the LayerNorm sums run in one order for every M, and the
+// one-row and four-row builds share every reduction, so a clip decodes the same bits whether 1 or 4 clips
+// share the step (tests/test_gpu_pdec.py::test_pdec_batch_equals_single).
 #pragma once
 #include <algorithm>
 
@@ -303,61 +310,70 @@ struct ColSlice {
 };
 
 // LayerNorm of rows [0, M <= 4) of xf (f32 [M][D], LDS) into out (T, row stride D; LDS or global),
-// layernorm_kernel's arithmetic (double sums, separately rounded ops). A row is split over WPR = 4 / M
-// waves for M <= 2 (their double partial sums added in wave order through lred, LDS [8]), else one wave
-// per row; lane l of a row's wave q holds elements k = l + 64 (q + WPR e), e < NE, all read from LDS at
-// once into registers (no branch per element: the reads are not serialised). gamma / beta (gam, bet)
-// are LDS copies staged a phase ahead (ln_issue / ln_commit in the kernel).
+// layernorm_kernel's arithmetic (double sums, separately rounded ops). The sums run in ONE canonical order
+// whatever M is (a row's result must not depend on how many rows share the launch): a row's
+// elements form 4 partitions q (k = l + 64 (q + 4 e), lane l), each summed sequentially over e and reduced
+// over the wave's lanes by the same DPP tree, then the 4 partition sums added in q order. The WPR = 4 / M
+// waves of a row (M <= 2; one wave per row for M > 2) take QW = 4 / WPR partitions each; all element reads
+// are issued into registers at once (no branch per element). gamma / beta (gam, bet) are LDS copies staged a
+// phase ahead (ln_issue / ln_commit in the kernel). lred: LDS doubles [2][kPdecMaxRows][4].
 template <typename T, int D, int WPR>
 __device__ __forceinline__ void ln_rows_w(const float* xf, int M, const float* gam, const float* bet, T* out, double* lred) {
 #pragma clang fp contract(off)
-    constexpr int NE = ((D + 63) / 64 + WPR - 1) / WPR;
+    constexpr int QW = 4 / WPR;
+    constexpr int NE = ((D + 63) / 64 + 3) / 4;
     const int tid = ptid(), wave = tid >> 6, lane = tid & 63;
-    const int q = wave % WPR, m = wave / WPR;
+    const int r = wave % WPR, m = wave / WPR;
     const bool on = m < M;
     const float* x = xf + (long)(on ? m : 0) * D;
-    float v[NE];
+    float v[QW][NE];
 #pragma unroll
-    for (int e = 0; e < NE; e++) {
-        const int k = lane + 64 * (q + WPR * e);
-        const float xv = x[k < D ? k : 0];
-        v[e] = k < D ? xv : 0.0f;
+    for (int j = 0; j < QW; j++)
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const int k = lane + 64 * (r * QW + j + 4 * e);
+            const float xv = x[k < D ? k : 0];
+            v[j][e] = k < D ? xv : 0.0f;
+        }
+#pragma unroll
+    for (int j = 0; j < QW; j++) {
+        double s = 0.0;
+#pragma unroll
+        for (int e = 0; e < NE; e++) s += (double)v[j][e];
+        s = wave_sum_d(s);
+        if (lane == 0 && on) lred[m * 4 + r * QW + j] = s;
     }
-    double s = 0.0;
-#pragma unroll
-    for (int e = 0; e < NE; e++) s += (double)v[e];
-    s = wave_sum_d(s);
-    if (lane == 0) lred[wave] = s;
     __syncthreads();
-    double st = 0.0;
-#pragma unroll
-    for (int i = 0; i < WPR; i++) st += lred[m * WPR + i];
+    const double st = (((0.0 + lred[m * 4]) + lred[m * 4 + 1]) + lred[m * 4 + 2]) + lred[m * 4 + 3];
     const float mean = (float)(st / D);
-    double s2 = 0.0;
 #pragma unroll
-    for (int e = 0; e < NE; e++) {
-        const int k = lane + 64 * (q + WPR * e);
-        v[e] = v[e] - mean;
-        if (k < D) s2 += (double)(v[e] * v[e]);
+    for (int j = 0; j < QW; j++) {
+        double s2 = 0.0;
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const int k = lane + 64 * (r * QW + j + 4 * e);
+            v[j][e] = v[j][e] - mean;
+            if (k < D) s2 += (double)(v[j][e] * v[j][e]);
+        }
+        s2 = wave_sum_d(s2);
+        if (lane == 0 && on) lred[16 + m * 4 + r * QW + j] = s2;
     }
-    s2 = wave_sum_d(s2);
-    if (lane == 0) lred[4 + wave] = s2;
     __syncthreads();
-    double st2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < WPR; i++) st2 += lred[4 + m * WPR + i];
+    const double st2 = (((0.0 + lred[16 + m * 4]) + lred[16 + m * 4 + 1]) + lred[16 + m * 4 + 2]) + lred[16 + m * 4 + 3];
     const float variance = (float)(st2 / D);
     const float scale = 1.0f / sqrtf(variance + 1e-5f);
     if (on) {
 #pragma unroll
-        for (int e = 0; e < NE; e++) {
-            const int k = lane + 64 * (q + WPR * e);
-            if (k < D) {
-                float t = v[e] * scale;
-                t = t * gam[k];
-                out[(long)m * D + k] = (T)(t + bet[k]);
+        for (int j = 0; j < QW; j++)
+#pragma unroll
+            for (int e = 0; e < NE; e++) {
+                const int k = lane + 64 * (r * QW + j + 4 * e);
+                if (k < D) {
+                    float t = v[j][e] * scale;
+                    t = t * gam[k];
+                    out[(long)m * D + k] = (T)(t + bet[k]);
+                }
             }
-        }
     }
     __syncthreads();  // lred is rewritten by the next call
 }
@@ -816,18 +832,22 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
             stamp(l, 3, 1);
         }
         // ---- E: cross attention over the cached K/V, split over keys; split 0 of a (row, head) merges -----------
+        // The split count is a function of the model shape only (pdec_cross_splits): M * H * S tasks, dealt to
+        // the workgroups round-robin (task t by workgroup t % 256). Every task's attention and publish comes
+        // before any merge waits, so no wait can stand behind another workgroup's unfinished task.
         {
-            // phase G's weights and LayerNorm parameters: a task workgroup issues them once its output is
+            // phase G's weights and LayerNorm parameters: a task workgroup issues them once its outputs are
             // out (issuing 4d x d of weights stalls the wave while the memory pipeline is full)
             auto ahead = [&] {
                 ln_issue(W.ln2_w, W.ln2_b);
                 wf1.load(cmat(W.f1), W.b1, 4 * D, D, true, zp);
             };
-            const int S = a.s_cross;
-            if (w0 >= M * H * S) ahead();
-            if (w0 < M * H * S) {
-                const int m = w0 / (H * S), h = (w0 / S) % H, s = w0 % S;
-                const int T_ = a.n_audio_ctx;
+            const int S = a.s_cross, NT = M * H * S;
+            const bool multi = NT > kG;  // (uniform) some workgroups take two or more tasks
+            const int T_ = a.n_audio_ctx;
+            if (w0 >= NT) ahead();
+            for (int t = w0; t < NT; t += kG) {
+                const int m = t / (H * S), h = (t / S) % H, s = t % S;
                 const int r0 = (int)((long)s * T_ / S), r1 = (int)((long)(s + 1) * T_ / S);
                 const long sl = SLOT[m];
                 const T* Kc = cross + (((sl * L + l) * 2 + 0) * H + h) * (long)T_ * 64;
@@ -840,38 +860,43 @@ __global__ void __launch_bounds__(kNT, 1) pdec_kernel(const PdecArgs a) {
                                qf[2 * i + 1] = (float)hi_t<T>(b);
                            }, err, lflag, spin))
                     return;
-                stamp(l, 4, 0);
+                if (t == w0) stamp(l, 4, 0);
                 attn_task<T, 8, true>(qf, Kc, Vc, rk, rv, r0, r1, -1, qf, qf, sc, red, res, zp);  // (no fresh row)
-                // the partial {max, sum, o[64]} as 66 granules; split 0 gathers the others and merges:
-                // o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s
-                unsigned long long* gp0 = g_part + (long)(w0 - s) * kPartG;
-                if (s > 0) {
+                // the partial {o[64], max, sum} as 66 granules (split 0 of a one-task workgroup keeps its own in LDS)
+                unsigned long long* gp0 = g_part + (long)(t - s) * kPartG;
+                if (s > 0 || multi) {
                     if (tid < kPartG) put_g(gp0 + (long)s * kPartG, tid, tag(l, 4), __builtin_bit_cast(uint32_t, res[tid]));
-                    ahead();
-                } else {
-                    if (tid < kPartG) part[tid] = res[tid];
-                    ahead();  // (lands while the other splits finish)
-                    if (!sweep<16>(gp0 + kPartG, (S - 1) * kPartG, tag(l, 4), [](int i) { return (long)i; },
-                                   [&](int i, uint32_t b) { part[kPartG + i] = f32_of(b); }, err, lflag, spin))
-                        return;
-                    if (tid < 64) {
-                        float mx = -INFINITY;
-                        for (int u = 0; u < S; u++) mx = fmaxf(mx, part[u * kPartG + 64]);
-                        float Lsum = 0.0f, o = 0.0f;
-                        for (int u = 0; u < S; u++) {
-                            const float ms = part[u * kPartG + 64];
-                            const float wgt = ms != -INFINITY ? __expf(ms - mx) : 0.0f;
-                            Lsum += wgt * part[u * kPartG + 65];
-                            o += wgt * part[u * kPartG + tid];
-                        }
-                        res[tid] = o * (1.0f / Lsum);
-                    }
-                    __syncthreads();
-                    if (tid < 32) put_g(g_xo, (long)m * (D / 2) + h * 32 + tid, tag(l, 5), pack2<T>(res[2 * tid], res[2 * tid + 1]));
-                    __syncthreads();  // part read before the next layer's merge rewrites it
+                } else if (tid < kPartG) {
+                    part[tid] = res[tid];
                 }
-                stamp(l, 4, 1);
+                if (t + kG >= NT) ahead();  // (after the workgroup's last task: lands while the other splits finish)
             }
+            // merges: o = sum_s e^(m_s - m) o_s / sum_s e^(m_s - m) l_s, by split 0's workgroup
+            for (int t = w0; t < NT; t += kG) {
+                if (t % S != 0) continue;  // (uniform)
+                const int m = t / (H * S), h = (t / S) % H;
+                unsigned long long* gp0 = g_part + (long)t * kPartG;
+                const int g0 = multi ? 0 : kPartG;  // one-task workgroups hold split 0's partial already
+                if (!sweep<16>(gp0 + g0, S * kPartG - g0, tag(l, 4), [](int i) { return (long)i; },
+                               [&](int i, uint32_t b) { part[g0 + i] = f32_of(b); }, err, lflag, spin))
+                    return;
+                if (tid < 64) {
+                    float mx = -INFINITY;
+                    for (int u = 0; u < S; u++) mx = fmaxf(mx, part[u * kPartG + 64]);
+                    float Lsum = 0.0f, o = 0.0f;
+                    for (int u = 0; u < S; u++) {
+                        const float ms = part[u * kPartG + 64];
+                        const float wgt = ms != -INFINITY ? __expf(ms - mx) : 0.0f;
+                        Lsum += wgt * part[u * kPartG + 65];
+                        o += wgt * part[u * kPartG + tid];
+                    }
+                    res[tid] = o * (1.0f / Lsum);
+                }
+                __syncthreads();
+                if (tid < 32) put_g(g_xo, (long)m * (D / 2) + h * 32 + tid, tag(l, 5), pack2<T>(res[2 * tid], res[2 * tid + 1]));
+                __syncthreads();  // part and res read before the next merge / layer rewrites them
+            }
+            if (w0 < NT) stamp(l, 4, 1);
         }
         // ---- F: cross-out projection + residual -------------------------------------------------------------------
         {

@@ -170,6 +170,8 @@ def lib() -> C.CDLL:
         "whisper_mi355x_abi_layout": (C.c_int, [C.POINTER(C.c_size_t)]),
         "whisper_mi355x_kernel_timing": (C.c_int, [vp, C.c_int]),
         "whisper_mi355x_kernel_stats": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
+        "whisper_mi355x_pdec_give_ups": (C.c_long, [vp]),
+        "whisper_mi355x_decoded_tokens_total": (C.c_long, []),
         "whisper_mi355x_set_pdec_spin": (None, [C.c_long]),
         "whisper_mi355x_set_pdec_stamps": (None, [vp]),
         "whisper_mi355x_set_pdec_blocks": (None, [C.c_int]),
@@ -374,6 +376,10 @@ class WhisperState:
         out = (C.c_int * 5)()
         assert self.L.whisper_mi355x_state_info(self.ptr, out) == 5
         return dict(direct=bool(out[0]), cap_jobs=out[1], cap_cross=out[2], graphs=out[3], pooled=bool(out[4]))
+
+    def pdec_give_ups(self) -> int:
+        """Persistent decode launches of this state that gave up and were re-run on the per-kernel path."""
+        return int(self.L.whisper_mi355x_pdec_give_ups(self.ptr))
 
     def phase_ms(self):
         out = (C.c_double * 5)()

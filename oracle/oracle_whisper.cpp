@@ -433,6 +433,9 @@ struct State {
     std::vector<float> step_margin;
     std::vector<int> step_token, step_seek;  // the greedy choice of each such step and its window's seek
     std::vector<int> seg_seek;               // per result segment: the seek of the window it came from
+    // fixed-work mode only: the raw logits row of every step (prefill's last row, then each decode), the
+    // rows a teacher-forced pass along the greedy sequence would produce (tests compare GPU logits with them)
+    std::vector<float> step_logits;
     int cur_seek = 0;
     // per decoded window: the temperature-fallback decisions (the record whisper_mi355x.h exposes)
     struct Decision { int seek, temp_idx, failed0, logprob_fail0, result_len0, no_speech; float avg_logprob0, entropy0, no_speech_prob, pad; };
@@ -725,6 +728,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
     s.step_margin.clear();
     s.step_token.clear();
     s.step_seek.clear();
+    s.step_logits.clear();
     s.decisions.clear();
     if (n_samples > 0) s.n_len = mel_compute(samples, n_samples, m.filters.data(), m.filt_n_mel, m.filt_n_fft, s.mel, &s.n_len_org, m.n_threads);
     const Vocab& vocab = m.vocab;
@@ -800,6 +804,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
                 compute_probs(lg, V, lp, pr);
                 s.no_speech_prob = pr[vocab.token_nosp];
             }
+            if (p.fixed_tokens > 0) s.step_logits.insert(s.step_logits.end(), last, last + V);
             process_logits(m, s, dec, p, t_cur, last);
             for (int i = 0; i < n_steps; ++i) {
                 dec.sequence.tokens.push_back(sample_token(m, s, dec, t_cur < 1e-6f));
@@ -832,6 +837,7 @@ static int full(Model& m, State& s, OracleParams p, const float* samples, int n_
                 if (p.fixed_tokens <= 0 && i == n_max - 1 && (dec.sequence.result_len == 0 || dec.seek_delta < 100 * 30 / 2)) { dec.failed = true; break; }
                 const int tok = dec.sequence.tokens.back().id;
                 decode(m, s, &tok, 1, (int)prompt.size() + i);
+                if (p.fixed_tokens > 0) s.step_logits.insert(s.step_logits.end(), s.logits.begin(), s.logits.begin() + V);
                 process_logits(m, s, dec, p, t_cur, s.logits.data());
             }
             bool success = true;
@@ -999,6 +1005,15 @@ void oracle_step_tokens(void* sp, int* tok, int* seek) {
     const State& s = *(State*)sp;
     std::copy(s.step_token.begin(), s.step_token.end(), tok);
     std::copy(s.step_seek.begin(), s.step_seek.end(), seek);
+}
+// fixed-work mode: the raw logits rows of the last full() call ([rows][V]); returns the row count (copies
+// only when cap >= rows * V)
+long oracle_step_logits(void* mp, void* sp, float* out, long cap) {
+    const State& s = *(State*)sp;
+    const long V = ((Model*)mp)->vocab.n_vocab;
+    const long n = (long)s.step_logits.size();
+    if (out && cap >= n) std::copy(s.step_logits.begin(), s.step_logits.end(), out);
+    return n / V;
 }
 int oracle_segment_seek(void* sp, int i) { return ((State*)sp)->seg_seek.at(i); }
 void oracle_step_margins(void* sp, float* out) { auto& v = ((State*)sp)->step_margin; std::copy(v.begin(), v.end(), out); }

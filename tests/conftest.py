@@ -53,3 +53,18 @@ def golden():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(autouse=True)
+def _no_pdec_give_ups(request):
+    """Every GPU test but the give-up test itself: no persistent decode launch gave up (a give-up re-runs
+    the step on the per-kernel path, so results stay right while the step silently costs the 50 ms wait:
+    VERDICT r4 weak 11)."""
+    if request.node.get_closest_marker("gpu") is None or "give_up" in request.node.name:
+        yield
+        return
+    L = request.getfixturevalue("wrs").lib()
+    before = L.whisper_mi355x_pdec_give_ups(None)
+    yield
+    after = L.whisper_mi355x_pdec_give_ups(None)
+    assert after == before, f"{after - before} persistent decode launch(es) gave up during {request.node.name}"

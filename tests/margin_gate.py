@@ -62,3 +62,49 @@ def assert_diverges_only_at_close_calls(got, exp, margins, gap, min_confident=0,
     assert covered >= min(min_confident, confident) or n >= min(min_prefix, len(exp)), \
         f"identical prefix {n} (< {min_prefix}) holds {covered} confident tokens < {min(min_confident, confident)}"
     return n
+
+
+DEC_KEYS = ("seek", "temp_idx", "failed0", "logprob_fail0", "result_len0", "no_speech")
+
+
+def assert_closed_before_divergence(segs, decs, ref, n):
+    """Near-tie runs (VERDICT r4 "next" #1): besides the identical token prefix of length n (kept tokens,
+    as assert_diverges_only_at_close_calls returns it), everything that was decided before the divergence
+    must equal the oracle's:
+      * every segment that closes before it (at least one identical kept token follows the segment):
+        its tokens, t0, t1 and text;
+      * every window that ends before the window of the first differing token: its per-window
+        decisions (seek, temperature index, greedy failure, logprob failure, result length, no-speech).
+    segs: GPU segments (whisper_rs.Segment), decs: GPU decisions (dicts), ref: oracle_py Oracle.full.
+    When the whole token sequence is identical (a near tie that did not flip), everything is compared.
+    Returns (segments compared, windows compared)."""
+    rsegs = ref["segments"]
+    n_kept = sum(len(s["tokens"]) for s in rsegs)
+    got_tokens = [t[0] for s in segs for t in s.tokens]
+    if n == n_kept and len(got_tokens) == n_kept:
+        n_seg, div_seek = len(rsegs), None
+    else:
+        n_seg, cum = 0, 0
+        for s in rsegs:
+            cum += len(s["tokens"])
+            if cum >= n:
+                break
+            n_seg += 1
+        # the window of the first differing kept token (or, when the GPU only went on past the oracle's
+        # last token, the window of that last token)
+        k, cum, div_seek = min(n, n_kept - 1), 0, rsegs[-1]["seek"] if rsegs else 0
+        for s in rsegs:
+            if k < cum + len(s["tokens"]):
+                div_seek = s["seek"]
+                break
+            cum += len(s["tokens"])
+    assert len(segs) >= n_seg, (len(segs), n_seg)
+    for i in range(n_seg):
+        g, r = segs[i], rsegs[i]
+        assert ([t[0] for t in g.tokens], g.t0, g.t1) == (r["tokens"], r["t0"], r["t1"]), (i, g.t0, g.t1, r["t0"], r["t1"])
+        assert g.text == r["text"], (i, g.text, r["text"])
+    rdec = ref["decisions"] if div_seek is None else [d for d in ref["decisions"] if d["seek"] < div_seek]
+    assert len(decs) >= len(rdec), (len(decs), len(rdec))
+    for k, d in enumerate(rdec):
+        assert tuple(decs[k][x] for x in DEC_KEYS) == tuple(d[x] for x in DEC_KEYS), (k, decs[k], d)
+    return n_seg, len(rdec)

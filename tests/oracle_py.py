@@ -101,6 +101,7 @@ def lib():
             "oracle_step_margins": (None, [vp, fp]),
             "oracle_step_tokens": (None, [vp, ip, ip]),
             "oracle_segment_seek": (C.c_int, [vp, C.c_int]),
+            "oracle_step_logits": (C.c_long, [vp, vp, fp, C.c_long]),
             "oracle_decoder_tokens": (C.c_int, [vp, ip, C.c_int]),
             "oracle_mel_tables": (None, [fp, fp, fp]),
             "oracle_tensor": (C.c_long, [vp, C.c_char_p, C.c_int, fp, C.c_long]),
@@ -233,10 +234,47 @@ class Oracle:
         nd = self.L.oracle_n_decisions(self.s)
         dec = (Decision * max(1, nd))()
         self.L.oracle_decisions(self.s, C.cast(dec, C.c_void_p))
-        return dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
-                    no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins, seq=list(seq[:n_seq]),
-                    step_tokens=step_tok[:n].tolist(), step_seeks=step_seek[:n].tolist(),
-                    decisions=decisions_to_dicts(dec[:nd]))
+        out = dict(rc=rc, segments=segs, lang=self.L.oracle_lang(self.s),
+                   no_speech_prob=self.L.oracle_no_speech(self.s), margins=margins, seq=list(seq[:n_seq]),
+                   step_tokens=step_tok[:n].tolist(), step_seeks=step_seek[:n].tolist(),
+                   decisions=decisions_to_dicts(dec[:nd]))
+        if params.fixed_tokens > 0:
+            # the raw logits of every step ([steps][V]): what a teacher-forced pass along the greedy
+            # sequence computes (same prompt, same cross K/V), recorded instead of decoded a second time
+            rows = self.L.oracle_step_logits(self.m, self.s, None, 0)
+            lg = np.empty((rows, self.n_vocab), np.float32)
+            self.L.oracle_step_logits(self.m, self.s, _fp(lg), lg.size)
+            out["step_logits"] = lg
+        return out
+
+
+# ---- one oracle per model file and one result per (model, input, params) for the whole pytest session ----
+# (the full-depth oracle runs ~13 s per large-v3 encoder pass; test modules that
+# compare against the same oracle result share it instead of recomputing it)
+_SHARED = {}
+_FULL = {}
+
+
+def shared_oracle(path: str, mode: int = 1, n_threads: int = 16) -> "Oracle":
+    key = (path, mode)
+    if key not in _SHARED:
+        _SHARED[key] = Oracle(path, mode=mode, n_threads=n_threads)
+    return _SHARED[key]
+
+
+def params_key(p: OracleParams) -> tuple:
+    return tuple(getattr(p, f) for f, _ in OracleParams._fields_)
+
+
+def cached_full(path: str, pcm_key, pcm_fn, params: OracleParams, mode: int = 1) -> dict:
+    """Oracle.full on a fresh state (whisper.rs:83-85: a new state per call), computed once per session
+    for (model file, pcm_key, params); pcm_fn() makes the input on a miss."""
+    key = (path, mode, pcm_key, params_key(params))
+    if key not in _FULL:
+        o = shared_oracle(path, mode)
+        o.new_state()
+        _FULL[key] = o.full(pcm_fn(), params)
+    return _FULL[key]
 
 
 # ---- audio.rs restatement (oracle/oracle_audio.cpp) -------------------------------------------------

@@ -18,7 +18,7 @@ import pytest
 
 from make_model import synthetic_pcm
 from margin_gate import assert_diverges_only_at_close_calls, kept_token_margins
-from oracle_py import Oracle, reference_params
+from oracle_py import cached_full, reference_params
 
 pytestmark = pytest.mark.gpu
 
@@ -28,19 +28,14 @@ BF16_GAP = 2.0      # tests/test_gpu_configs.py: bf16 teacher-forced logits with
 FP8_GAP = 4.0
 MIN_CONFIDENT = 4  # tokens decided by > the gap that the identical prefix must hold
 
-_ORACLE = {}
 
 
 def oracle_full(shape, seed, t_inc=0.0, seconds=30.0):
     from conftest import model_path
-    key = (shape, seed, t_inc, seconds)
-    if key not in _ORACLE:
-        o = Oracle(model_path(shape), mode=1, n_threads=16)
-        rp = reference_params("en")
-        rp.temperature_inc = t_inc
-        _ORACLE[key] = o.full(synthetic_pcm(seed, seconds=seconds), rp)
-        o.close()
-    return _ORACLE[key]
+    rp = reference_params("en")
+    rp.temperature_inc = t_inc
+    key = ("clip", seed) if seconds == 30.0 else ("clip", seed, seconds)
+    return cached_full(model_path(shape), key, lambda: synthetic_pcm(seed, seconds=seconds), rp)
 
 
 def seg_full(segs):
@@ -113,13 +108,27 @@ def test_turbo_bf16_256_equals_two_128(wrs, monkeypatch):
     assert sum(len(b) for b in big) > 256  # every clip produced segments
 
 
+FP8_TF_TOL = 4.0   # |dlogit| bar of the teacher-forced fp8 check (the full-depth test's FP8_DEEP_TOL)
+FP8_SPOT = (0, 37, 64, 101, 128, 170, 203, 255)
+N_TF = 32          # teacher-forced steps per spot clip
+
+
 def test_turbo_fp8_b256_vs_oracle(wrs):
     """BASELINE configs[4]: large-v3-turbo with fp8 weights (e4m3 encoder GEMMs) at batch 256 (direct
-    cross attention, two decode row groups); 8 spot clips against the f16-numerics oracle: identical
-    up to the first step the oracle decided by <= FP8_GAP nats; over the spot clips together at least
-    half of the oracle's tokens identical before the first divergence."""
+    cross attention, two concurrent 128-clip halves); 8 spot clips against the f16-numerics oracle.
+    (1) greedy whisper_full: each clip identical up to the first step the oracle decided by <= FP8_GAP
+        nats. On this 2-layer-encoder shape the oracle decides most steps by < 1 nat (1 of a clip's ~11
+        kept tokens exceeds FP8_GAP), so a clip may legitimately diverge at its second token: the greedy
+        run alone holds little per-clip evidence, and round 4's floor over the 8 clips together (half of
+        the tokens) is replaced by (2).
+    (2) per clip (round 5, VERDICT r4 "next" #2): the same 256-clip call teacher-forced along the oracle's
+        fixed-work greedy sequence of each spot clip (whisper_mi355x_full_batch_forced, the same kernels):
+        max_v |dlogit| <= FP8_TF_TOL at every one of N_TF steps, and the argmax agrees wherever the
+        oracle's top-2 gap exceeds 2 * FP8_TF_TOL. The full 32-layer encoder depth:
+        tests/test_gpu_fulldepth.py::test_turbo_fp8_b256_teacher_forced."""
     from conftest import model_path
-    path = model_path("large-v3-turbo-2L+conf")
+    shape = "large-v3-turbo-2L+conf"
+    path = model_path(shape)
     seeds = [k % 64 for k in range(256)]
     clips = [synthetic_pcm(s) for s in seeds]
     p = wrs.reference_full_params("en")
@@ -129,17 +138,36 @@ def test_turbo_fp8_b256_vs_oracle(wrs):
     assert st.full_batch(p, clips) == 0
     assert st.info()["direct"]
     prefixes = []
-    for j in (0, 37, 64, 101, 128, 170, 203, 255):
-        ref = oracle_full("large-v3-turbo-2L+conf", seeds[j])
+    for j in FP8_SPOT:
+        ref = oracle_full(shape, seeds[j])
         exp, margins = kept_token_margins(ref)
         got = seg_tokens(st.batch_segments(j))
         prefixes.append((j, assert_diverges_only_at_close_calls(got, exp, margins, FP8_GAP), len(exp)))
+    print("fp8 b256 identical prefixes (clip, tokens, of):", prefixes)
+    # (2) teacher-forced logits of every spot clip
+    refs = [cached_full(path, ("clip", seeds[j]), lambda s=seeds[j]: synthetic_pcm(s), reference_params("en", fixed_tokens=N_TF))
+            for j in FP8_SPOT]
+    forced = np.array([refs[0]["step_tokens"]] * 256, np.int32)
+    for k, j in enumerate(FP8_SPOT):
+        forced[j] = refs[k]["step_tokens"]
+    V = wrs.lib().whisper_n_vocab(ctx.ptr)
+    rc, lg = st.full_batch_forced(wrs.reference_full_params("en"), clips, N_TF, forced, list(FP8_SPOT), V)
+    assert rc == 0, rc
     st.close()
     ctx.close()
-    print("fp8 b256 identical prefixes (clip, tokens, of):", prefixes)
-    # e4m3 operands flip close calls early more often than bf16: the floor is on the spot clips
-    # together, half of the oracle's tokens identical before the first divergence
-    assert sum(p[1] for p in prefixes) >= 0.5 * sum(p[2] for p in prefixes), prefixes
+    worst = []
+    for k, j in enumerate(FP8_SPOT):
+        ref = refs[k]["step_logits"].astype(np.float64)
+        got = lg[:, k, :].astype(np.float64)
+        assert np.isfinite(got).all()
+        per_step = np.abs(got - ref).max(axis=1)
+        top2 = np.sort(ref, axis=1)[:, -2:]
+        gap = top2[:, 1] - top2[:, 0]
+        flips = [(i, float(gap[i])) for i in range(N_TF) if int(np.argmax(got[i])) != int(np.argmax(ref[i]))]
+        worst.append((j, round(float(per_step.max()), 3), flips))
+        assert per_step.max() <= FP8_TF_TOL, (j, per_step.max(), int(per_step.argmax()))
+        assert all(g <= 2 * FP8_TF_TOL for _, g in flips), (j, flips)
+    print("fp8 b256 teacher-forced worst |dlogit| per spot clip (clip, worst, argmax flips):", worst)
 
 
 def test_largev3_bf16_b128_direct_vs_oracle(wrs, monkeypatch):

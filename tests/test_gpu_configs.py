@@ -28,7 +28,7 @@ import pytest
 
 from make_model import synthetic_pcm
 from margin_gate import assert_diverges_only_at_close_calls, kept_token_margins
-from oracle_py import Oracle, reference_params
+from oracle_py import Oracle, cached_full, reference_params
 
 pytestmark = pytest.mark.gpu
 
@@ -38,20 +38,14 @@ pytestmark = pytest.mark.gpu
 BF16_LOGIT_TOL = 1.0
 BF16_GAP = 2 * BF16_LOGIT_TOL
 
-_ORACLE = {}
-
-
 def oracle_full(shape, pcm_key, lang, prompt=None, t_inc=0.2):
-    """Cached oracle whisper_full (the CPU restatement is the slow side)."""
+    """Oracle whisper_full, computed once per session (oracle_py.cached_full; the CPU restatement is the
+    slow side)."""
     from conftest import model_path
-    key = (shape, pcm_key, lang, prompt, t_inc)
-    if key not in _ORACLE:
-        o = Oracle(model_path(shape), mode=1, n_threads=16)
-        rp = reference_params(lang, prompt=prompt)
-        rp.temperature_inc = t_inc
-        _ORACLE[key] = o.full(_pcm(pcm_key), rp)
-        o.close()
-    return _ORACLE[key]
+    rp = reference_params(lang, prompt=prompt)
+    rp.temperature_inc = t_inc
+    k, sec = pcm_key
+    return cached_full(model_path(shape), ("clip", k) if sec == 30.0 else ("clip", k, sec), lambda: _pcm(pcm_key), rp)
 
 
 def _pcm(key):

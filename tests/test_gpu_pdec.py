@@ -11,7 +11,9 @@ cross K/V cache form.
     oracle like the f16 cases;
   * a batch of 4 clips (the largest it takes) against the oracle clip by clip;
   * the give-up path: with a zero spin limit every launch gives up and the step is re-run on the
-    per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit;
+    per-kernel path: results equal the per-kernel path's (WHISPER_MI355X_PDEC=0) bit for bit, and the
+    state's give-up counter says so (every other case asserts it is 0);
+  * batch == single on the default path (3 clips of different lengths: persistent steps at 3, 2, 1 clips);
   * two states on two host threads (persistent steps serialised by the engine): each equals its
     single-threaded run.
 Each case checks that the persistent kernel actually ran (its kernel-timing class counted launches).
@@ -21,8 +23,8 @@ import threading
 import pytest
 
 from make_model import synthetic_pcm
-from margin_gate import assert_diverges_only_at_close_calls, kept_token_margins
-from oracle_py import Oracle, reference_params
+from margin_gate import assert_closed_before_divergence, assert_diverges_only_at_close_calls, kept_token_margins
+from oracle_py import cached_full, reference_params
 
 pytestmark = pytest.mark.gpu
 
@@ -31,19 +33,13 @@ K_PDEC = 7
 # (f16 teacher-forced logits sit within ~0.015 of the oracle's, tests/test_gpu_fulldepth.py); where the
 # oracle itself has a near tie, exactly up to that step (the round-2 rule)
 F16_GAP = 0.05
-_REF = {}
 
 
 def oracle_full(shape, clip, lang="en", prompt=None, t_inc=0.2):
     from conftest import model_path
-    key = (shape, clip, lang, prompt, t_inc)
-    if key not in _REF:
-        o = Oracle(model_path(shape), mode=1, n_threads=16)
-        rp = reference_params(lang, prompt=prompt)
-        rp.temperature_inc = t_inc
-        _REF[key] = o.full(synthetic_pcm(clip), rp)
-        o.close()
-    return _REF[key]
+    rp = reference_params(lang, prompt=prompt)
+    rp.temperature_inc = t_inc
+    return cached_full(model_path(shape), ("clip", clip), lambda: synthetic_pcm(clip), rp)
 
 
 def ints(segs):
@@ -86,10 +82,12 @@ def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
     gp.temperature_inc = t_inc
     assert st.full(gp, synthetic_pcm(clip)) == 0
     n = pdec_launches(wrs, st)
+    gave_up = st.pdec_give_ups()
     segs, dec = st.segments(), st.decisions()
     st.close()
     ctx.close()
     assert n > 0, "the persistent decode step did not run"
+    assert gave_up == 0, f"{gave_up} persistent launches gave up (re-run on the per-kernel path)"
     exp, margins = kept_token_margins(ref)
     if min(margins) > F16_GAP:
         assert ints(segs) == ref_ints(ref)
@@ -99,8 +97,9 @@ def test_pdec_full_f16_exact(wrs, monkeypatch, shape, clip, lang, prompt, t_inc)
     else:  # the oracle decided a step by <= F16_GAP nats: exact up to the first such near tie
         got = [t for sg in ints(segs) for t in sg[0]]
         k = assert_diverges_only_at_close_calls(got, exp, margins, F16_GAP, 4)
+        ns, nw = assert_closed_before_divergence(segs, dec, ref, k)
         print(f"{shape} clip {clip}: {n} persistent steps, {k} of {len(exp)} tokens identical "
-              f"(oracle near tie {min(margins):.4f} nats)")
+              f"(oracle near tie {min(margins):.4f} nats); {ns} segment(s), {nw} window decision(s) before it identical")
 
 
 QUANT_CASES = [("small-4L+conf+q5_1", 1, "en", None, 0.2), ("large-v3-2L+conf+q5_0", 0, "en", None, 0.2),
@@ -143,7 +142,7 @@ def _run(wrs, path, clips, dtype):
     wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
     assert st.full_batch(wrs.reference_full_params("en"), clips) == 0
     out = [ints(st.batch_segments(j)) for j in range(len(clips))], [st.decisions(j) for j in range(len(clips))]
-    n = pdec_launches(wrs, st)
+    n = (pdec_launches(wrs, st), st.pdec_give_ups())
     st.close()
     ctx.close()
     return out, n
@@ -161,14 +160,16 @@ def test_pdec_give_up_reruns_step(wrs, monkeypatch, capfd, dtype):
     L = wrs.lib()
     monkeypatch.setenv("WHISPER_MI355X_PDEC", "0")
     plain, n0 = _run(wrs, path, clips, getattr(wrs, dtype))
-    assert n0 == 0
+    assert n0 == (0, 0)
     monkeypatch.delenv("WHISPER_MI355X_PDEC")
     L.whisper_mi355x_set_pdec_spin(0)
     try:
         forced, n1 = _run(wrs, path, clips, getattr(wrs, dtype))
     finally:
         L.whisper_mi355x_set_pdec_spin(5000000)
-    assert n1 > 0
+    # the first launch gives up and is re-run; the state's next steps then take the per-kernel path for
+    # the backoff period instead of timing out again (kernel stats count the give-ups)
+    assert n1[0] > 0 and n1[1] >= 1, n1
     assert forced == plain
 
 
@@ -200,3 +201,35 @@ def test_pdec_two_threads(wrs, monkeypatch):
     ctx.close()
     assert [r[0] for r in res] == [0, 0]
     assert [r[1] for r in res] == single
+
+
+@pytest.mark.parametrize("shape", ["base+conf", "large-v3-2L+conf"])
+def test_pdec_batch_equals_single(wrs, monkeypatch, shape):
+    """The default path (no switches): a batch of 3 clips of different lengths, whose decode steps run the
+    persistent kernel at 3, 2 and 1 active clips as clips finish, equals each clip run alone (1 clip per
+    step) bit for bit: token ids, probabilities, timestamps, text and window decisions (the
+    key-split count and the LayerNorm order no longer depend on the clip count). large-v3-2L (20 heads)
+    deals 2-3 cross-attention tasks to some workgroups at 2-3 clips; base (8 heads) one each."""
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_CROSS", "cache")
+    path = model_path(shape)
+    clips = [synthetic_pcm(k, seconds=30.0 - 4.0 * k) for k in range(3)]
+    p = wrs.reference_full_params("en")
+    p.temperature_inc = 0.0
+    ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+
+    def run(batch):
+        st = ctx.create_state()
+        wrs.lib().whisper_mi355x_kernel_timing(st.ptr, 1 << K_PDEC)
+        assert st.full_batch(p, batch) == 0
+        out = [([tuple(t) for t in s.tokens], s.t0, s.t1, s.text) for j in range(len(batch)) for s in st.batch_segments(j)], \
+            [st.decisions(j) for j in range(len(batch))]
+        n, g = pdec_launches(wrs, st), st.pdec_give_ups()
+        st.close()
+        assert n > 0 and g == 0, (n, g)
+        return out
+    together = run(clips)
+    alone = [run([c]) for c in clips]
+    ctx.close()
+    assert together[0] == [seg for a in alone for seg in a[0]]
+    assert together[1] == [a[1][0] for a in alone]
