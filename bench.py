@@ -35,8 +35,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "audio-sec/s (RTF⁻¹) large-v3 greedy, batch 128; 1/2/4/8 MI355X"
 K_NAMES = ["gemm_encoder", "attn_encoder", "attn_cross_decode", "attn_self_decode", "gemm_decode", "logits", "mel",
-           "pdec_step"]
-K_BOUND = ["mfma", "mfma", "hbm", "hbm", "hbm", "hbm", "hbm", "hbm"]
+           "pdec_step", "bdec_chain"]
+K_BOUND = ["mfma", "mfma", "hbm", "hbm", "hbm", "hbm", "hbm", "hbm", "hbm"]
 SINGLE_KERNEL = [1, 2, 3, 5, 6, 7]  # classes that are one kernel each (attention, logits, mel, persistent step)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0       # dense bf16/f16 MFMA peak (no sparsity)
@@ -501,7 +501,7 @@ def main():
 
     params = wrs.reference_full_params("en")
     # warmup (untimed) with every kernel class timed once to find the dominant kernel
-    L.whisper_mi355x_kernel_timing(st.ptr, 0xFF)
+    L.whisper_mi355x_kernel_timing(st.ptr, 0x1FF)
     tw = time.time()
     for _ in range(args.warmup):
         step(params)
@@ -522,7 +522,7 @@ def main():
     # BENCH_KTIME=0: no event pair inside the timed steps (A/B of the instrumentation's own cost)
     # per-layer decode attention classes are sampled every KT_LAYER_STRIDE-th layer: an event pair per
     # launch in all 32 layers cost ~2 % of the step at 128 clips and ~5 % at 16 (BENCH_KTIME=0 A/B)
-    mask = (1 << dom) | ((KT_LAYER_STRIDE << 8) if dom in (2, 3) else 0)
+    mask = (1 << dom) | ((KT_LAYER_STRIDE << 16) if dom in (2, 3) else 0)
     L.whisper_mi355x_kernel_timing(st.ptr, 0 if os.environ.get("BENCH_KTIME") == "0" else mask)
     elapsed = timed(params, args.steps)
     out = (C.c_double * 3)()

@@ -70,6 +70,13 @@ WHISPER_API long whisper_mi355x_batch_decoded_tokens(struct whisper_state * stat
 /* tokens generated by every whisper_full / whisper_mi355x_full_batch call of the process so far (lets a
  * caller that drives whisper.h through its own states, e.g. the WhisperEngine mirror, count per call) */
 WHISPER_API long whisper_mi355x_decoded_tokens_total(void);
+/* Debug: the batched persistent decoder chain's hand-off counters and error word after the state's last
+ * decode step (u32 words, out must hold them); returns the word count (-count if cap is too small). */
+WHISPER_API int whisper_mi355x_debug_bdec_sync(struct whisper_state * state, unsigned * out, int cap);
+/* Debug: device pointers of a state's decode workspace (0 residual x, 1 final LayerNorm rows, 2 q|k|v rows of
+ * the batched chain, 3 attention outputs, 4 GELU rows, 5 cross q, 6 Q', 7 cross-attention partials, 8 their
+ * {m, l}); NULL when not allocated. */
+WHISPER_API void * whisper_mi355x_debug_ws(struct whisper_state * state, int which);
 
 /* Per-window decisions of whisper_full's temperature-fallback loop (the integer outcomes that are
  * comparable with whisper.cpp even when a sampled t > 0 attempt is not): one record per decoded
@@ -107,8 +114,9 @@ WHISPER_API int whisper_mi355x_get_encoder_out(struct whisper_state * state, flo
 /* Live per-kernel-class timing with HIP events on the state's stream (used by bench.py for the
  * roofline). Classes: 0 encoder-side GEMM (work = FLOPs), 1 encoder attention (FLOPs),
  * 2 decoder cross-attention (HBM bytes), 3 decoder self-attention (bytes), 4 decoder GEMM (bytes),
- * 5 logits processing (bytes), 6 mel (bytes). class_mask bit k times class k (0 = off); bits 8..15,
- * when > 1, time the decoder's per-layer attention launches (classes 2, 3) of every k-th layer only.
+ * 5 logits processing (bytes), 6 mel (bytes), 7 the persistent decode step (bytes), 8 the batched
+ * persistent decoder chain (bytes). class_mask bit k times class k (0 = off); bits 16..23, when > 1, time
+ * the decoder's per-layer attention launches (classes 2, 3) of every k-th layer only.
  * Every call resets the counters; stats out = {total ms, launches, total work}. */
 WHISPER_API int whisper_mi355x_kernel_timing(struct whisper_state * state, int class_mask);
 WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cls, double out[3]);

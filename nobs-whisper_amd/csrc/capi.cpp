@@ -567,6 +567,24 @@ void whisper_mi355x_set_pdec_stamps(void* dev) {
     wm::g_pdec_stamps = (unsigned long long*)dev;
     wm::g_pdec_gen++;
 }
+// debug: the batched chain's counter block of the state's last step (u32 words) -> host; returns the word count
+int whisper_mi355x_debug_bdec_sync(struct whisper_state* s, unsigned* out, int cap) {
+    if (!s || !s->ctx || !s->ws.bd_sync) return -1;
+    const int n = (int)(wm::bdec_sync_bytes(s->ctx->hp.n_text_layer) / 4);
+    if (cap < n) return -n;
+    hipSetDevice(s->device);
+    if (hipStreamSynchronize(s->stream) != hipSuccess) return -1;
+    if (hipMemcpy(out, s->ws.bd_sync, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
+// debug: device pointers of the state's decode workspace: 0 x (f32 [rows][d]), 1 final LN rows, 2 q|k|v rows of
+// the chain, 3 attention outputs, 4 GELU rows, 5 cross q, 6 Q', 7 cross partials, 8 their {m, l}
+void* whisper_mi355x_debug_ws(struct whisper_state* s, int which) {
+    if (!s) return nullptr;
+    const wm::Workspace& w = s->ws;
+    void* p[9] = {w.dx, w.dh, w.bq, w.datt, w.dff, w.dq, w.qx, w.xo, w.xml};
+    return which >= 0 && which < 9 ? p[which] : nullptr;
+}
 long whisper_mi355x_decoded_tokens_total(void) { return wm::g_decoded_tokens_total.load(); }
 long whisper_mi355x_pdec_give_ups(struct whisper_state* s) { return s ? s->pdec_give_ups : wm::g_pdec_give_ups_total.load(); }
 void whisper_mi355x_set_pdec_blocks(int on) { wm::g_pdec_blocks = on != 0; }

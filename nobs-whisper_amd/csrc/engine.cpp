@@ -295,7 +295,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync); dfree(w.bd_sync); dfree(w.bq);
     if (w.h_pd_err) hipHostFree(w.h_pd_err);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
@@ -382,7 +382,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
         dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.mel_ptrs);
-        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles);
+        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles); dfree(w.bq);
         for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
             if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
         w.cap_jobs = w.cap_tok = w.cap_cross = w.cap_xq = 0;
@@ -839,9 +839,11 @@ static int pdec_max() {
 }
 
 // The per-call switches that choose a decode step's kernels, folded into the key of its captured graph.
+static bool bdec_on();
 static int dec_path_sig() {
     return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) |
-           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26) | ((g_pdec_blocks & 1) << 29);
+           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26) | ((g_pdec_blocks & 1) << 29) |
+           ((bdec_on() ? 1 : 0) << 30);
 }
 
 // Quantized files: the persistent step reads the context's expanded compute-type copy when it exists
@@ -948,6 +950,120 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
         launch_pdec(c->dt, a, st);
     }
     WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + a.gr.err_bytes, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
+    tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
+}
+
+// The batched persistent chain (kernels/bdec.hip) for decode steps of 5..128 clips in the direct cross form:
+// per layer one chain launch around the pass over E, instead of ~16 launches (VERDICT r4 "next" #3).
+// WHISPER_MI355X_BDEC=0 turns it off (read per call). Not while another call of this process is inside
+// full_batch (a second state, the twin half of a paired batch): the chain needs its 256 workgroups resident
+// together, and two such launches on two streams could each hold half the CUs.
+std::atomic<int> g_calls_in_flight{0};
+static bool bdec_on() {
+    const char* e = getenv("WHISPER_MI355X_BDEC");
+    return e && atoi(e) != 0;  // (opt-in until it beats the launch chain at every clip count)
+}
+static bool bdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
+    if (!xdirect || s->pdec_block || s->pdec_off || !bdec_on() || n < 5 || n > 128 || s->step_rows > 128) return false;
+    if (c->fp8_enc && !c->dec8.empty()) return false;
+    if (c->quant && !c->expanded.load(std::memory_order_acquire)) return false;
+    if (!bdec_supported(c->hp.n_text_state) || c->hp.n_text_state != 64 * c->hp.n_text_head) return false;
+    if (!c->w.wkT || g_calls_in_flight.load() > 1) return false;
+    static const int cus = [] {
+        int dev = 0, v = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+        return v;
+    }();
+    return cus == 256;
+}
+
+// Device array of the decoder layers' pointers for the chain (once per context)
+static const BdecLayer* bdec_layers(Context* c) {
+    std::lock_guard<std::mutex> lk(c->pdec_mu);
+    if (!c->bdec_layers) {
+        const int d = c->hp.n_text_state, H = c->hp.n_text_head;
+        std::vector<BdecLayer> h(c->hp.n_text_layer);
+        for (int l = 0; l < c->hp.n_text_layer; l++) {
+            const LayerW& L = c->w.dec[l];
+            LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
+            if (c->quant) m = c->exp_dec[l];
+            BdecLayer b{};
+            b.wqkv = m.wqkv; b.wo = m.wo; b.wxq = m.wxq; b.wxo = m.wxo; b.w1 = m.w1; b.w2 = m.w2;
+            b.wv = (const char*)c->w.wkv_cross + (size_t)(2 * l + 1) * d * d * 2;
+            b.wkt = (const char*)c->w.wkT + (size_t)l * H * d * 64 * 2;
+            b.bqkv = L.bqkv; b.bo = L.bo; b.bxq = L.bxq; b.bxo = L.bxo; b.b1 = L.b1; b.b2 = L.b2;
+            b.bv = c->w.bkv_cross + (size_t)(2 * l + 1) * d;
+            b.ln1_w = L.ln1_w; b.ln1_b = L.ln1_b; b.lnx_w = L.lnx_w; b.lnx_b = L.lnx_b; b.ln2_w = L.ln2_w; b.ln2_b = L.ln2_b;
+            h[l] = b;
+        }
+        void* p = nullptr;
+        WM_CHECK(hipMalloc(&p, h.size() * sizeof(BdecLayer)));
+        WM_CHECK(hipMemcpy(p, h.data(), h.size() * sizeof(BdecLayer), hipMemcpyHostToDevice));
+        c->bdec_layers = p;
+    }
+    return (const BdecLayer*)c->bdec_layers;
+}
+
+// Everything the chain allocates, before a decode step is captured
+static void bdec_prepare(Context* c, whisper_state* s) {
+    Workspace& w = s->ws;
+    bdec_layers(c);
+    if (!w.bd_sync) dalloc(w.bd_sync, bdec_sync_bytes(c->hp.n_text_layer));
+    if (!w.bq) dalloc(w.bq, (size_t)w.cap_jobs * 3 * c->hp.n_text_state * esize(c->dt));
+    if (!w.h_pd_err) {
+        WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
+        *w.h_pd_err = 0;
+    }
+}
+
+// One decode step of the view's rows: the chain's launches around the passes over E, then the logits GEMM
+// (graph-capturable). The error word goes to the host as a node of the step's graph (decode_step re-runs the
+// step on the per-kernel path if a launch gave up).
+static void decoder_rows_bdec(Context* c, whisper_state* s, const DecView& v, int kt_stride) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab, n = v.n, Ta = hp.n_audio_ctx;
+    hipStream_t st = v.st;
+    if (!w.bd_sync || !w.bq) WM_FAIL("bdec: buffers not allocated (bdec_prepare)");
+    const int S = xattn_splits(n, Ta);
+    BdecArgs a{};
+    a.layers = bdec_layers(c);
+    a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.S = S;
+    a.tok_emb = c->w.tok_emb_f32 ? (const void*)c->w.tok_emb_f32 : c->w.tok_emb;
+    a.te_f32 = c->w.tok_emb_f32 != nullptr;
+    a.pos_d = c->w.pos_d;
+    a.lnd_w = c->w.lnd_w; a.lnd_b = c->w.lnd_b;
+    a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
+    a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
+    a.self_cache = w.self; a.k_scale = c->k_scale;
+    a.x = w.dx + (size_t)v.r0 * d;
+    a.bq = w.bq; a.batt = w.datt; a.bff = w.dff; a.bxq = w.dq; a.qx = w.qx;
+    a.opart = v.xo; a.ml = v.xml;
+    a.cnt = w.bd_sync; a.err_index = bdec_err_index(L);
+    a.spin_ticks = g_pdec_spin_ticks;
+    a.gelu_tab = gelu_table_device();
+    a.dbg_fence = getenv("WHISPER_MI355X_BDEC_FENCE") ? atoi(getenv("WHISPER_MI355X_BDEC_FENCE")) : 0;
+    a.dbg_head_only = getenv("WHISPER_MI355X_BDEC_HEAD_ONLY") ? atoi(getenv("WHISPER_MI355X_BDEC_HEAD_ONLY")) : 0;
+    a.stamps = g_pdec_stamps;
+    WM_CHECK(hipMemsetAsync(w.bd_sync, 0, bdec_sync_bytes(L), st));
+    // weights once (14 d^2 per layer) + the rows' activations, per launch ~ one layer's worth
+    const double lbytes = 14.0 * d * d * 2 + (double)n * d * 4 * 16;
+    for (int l = -1; l < L; l++) {
+        a.la = l;
+        a.lb = l + 1;
+        {
+            KT kt(s, K_BDEC, lbytes, st);
+            launch_bdec(c->dt, a, st);
+        }
+        if (l + 1 < L) {
+            const bool kt_layer = (l + 1) % kt_stride == 0;
+            KT kt(s, K_ATTN_CROSS, (double)n * Ta * d * 2, st, kt_layer);
+            launch_xattn_step(c->dt, w.enc, a.slot, w.qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st);
+        }
+    }
+    WM_CHECK(hipMemcpyAsync(w.h_pd_err, w.bd_sync + bdec_err_index(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
     tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }
@@ -1093,9 +1209,13 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     };
     // kernel timing (bench roofline): bits 8..15 of the mask = time the per-layer attention launches of
     // every k-th layer only (fewer event nodes in the timed decode graphs; every layer does the same work)
-    const int kt_stride = std::max(1, (s->ktime_mask >> 8) & 0xFF);
+    const int kt_stride = std::max(1, (s->ktime_mask >> 16) & 0xFF);
     if (fused && pdec_use(c, s, n_tok, xdirect)) {
         decoder_rows_pdec(c, s, v);
+        return;
+    }
+    if (fused && bdec_use(c, s, n_tok, xdirect)) {
+        decoder_rows_bdec(c, s, v, kt_stride);
         return;
     }
     // (the persistent and small-M paths embed the tokens themselves)
@@ -1226,6 +1346,7 @@ static void decoder_launch(Context* c, whisper_state* s, int n_tok, int n_rows, 
     Workspace& w = s->ws;
     const bool step = rows_identity && n_rows == n_tok;  // a decode step: one token per clip, logits of every row
     const int groups = step ? dec_groups(n_tok) : 1;
+    s->step_rows = n_tok;
     if (groups == 1) {
         // prefill / language detection / whisper_decode: the unfused pass over the tiles that
         // decoder_upload built (decoder_forward); decode steps of <= 128 clips: one fused pass
@@ -1622,8 +1743,10 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     const int sig = dec_path_sig();
     const double t_step = now_ms();
     s->pdec_off = s->pdec_give_ups > 0 && t_step < s->pdec_off_until;
-    const bool pd = pdec_use(c, s, n, s->direct);
-    if (pd) pdec_prepare(c, s);
+    s->step_rows = n;
+    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
+    if (pd == 1) pdec_prepare(c, s);
+    if (pd == 2) bdec_prepare(c, s);
     // retire persistent-step graphs captured under an older stamps pointer / spin limit (g_pdec_gen)
     for (size_t i = 0; i < s->dec_graphs.size();) {
         auto& g = s->dec_graphs[i];
@@ -1658,9 +1781,9 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         kt_flush_graph(s, *G);
         return;
     }
-    // A persistent launch needs its 256 workgroups resident together: persistent steps of different
-    // states (threads) of this process on one device never overlap, so two of them cannot hold half the
-    // CUs each (steps on different devices do not wait for each other)
+    // A persistent launch (the one-launch step, or the chain's launches) needs its 256 workgroups resident
+    // together: persistent steps of different states (threads) of this process on one device never overlap,
+    // so two of them cannot hold half the CUs each (steps on different devices do not wait for each other)
     static std::mutex pdec_run_mu[16];
     bool gave_up;
     {
@@ -1796,6 +1919,10 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
         warned = true;
     }
     ensure_expanded(c, s->stream);  // quantized files: before anything is captured
+    struct InFlight {  // calls of this process inside full_batch (bdec_use)
+        InFlight() { g_calls_in_flight++; }
+        ~InFlight() { g_calls_in_flight--; }
+    } in_flight;
     Sched S;
     S.c = c; S.s = s; S.p = p; S.o = o; S.single_api = single_api;
     const Vocab& v = c->vocab;

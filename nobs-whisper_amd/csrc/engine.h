@@ -115,6 +115,7 @@ struct Context {
     std::mutex pdec_mu;
     void* pdec_layers = nullptr;
     void* pdec_layers_exp = nullptr;  // (a quantized file's expanded copy)
+    void* bdec_layers = nullptr;      // the batched chain's layer descriptors (kernels/bdec.hip)
     // States released by whisper_free_state, kept with their workspace and captured decode graphs
     // for the next whisper_init_state: whisper.rs:83-85 creates (and drops) a state on every
     // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.
@@ -170,8 +171,12 @@ struct Workspace {
     void* lrec = nullptr;  // split logits kernel: per-chunk records
     int *win_job = nullptr, *win_seek = nullptr, *win_slot = nullptr;
     // persistent decode step: the hand-off block (granules + error word) and the error word's host copy
+    // (shared with the batched chain's error word)
     unsigned* pd_sync = nullptr;
     unsigned* h_pd_err = nullptr;
+    // batched persistent chain (kernels/bdec.hip): its counters + error word, and the q|k|v rows [cap][3d]
+    unsigned* bd_sync = nullptr;
+    void* bq = nullptr;
     // mel / pcm
     float* pcm = nullptr;
     float* mel = nullptr;
@@ -191,7 +196,7 @@ struct Job;
 
 // Live per-kernel-class timing with HIP events on the state's stream (bench.py's roofline leg).
 // `work` is the algorithmic FLOPs (MFMA-bound classes) or HBM bytes (HBM-bound classes).
-enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_PDEC, K_OTHER, K_NCLASS };
+enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_PDEC, K_BDEC, K_OTHER, K_NCLASS };
 struct KStat { double ms = 0, work = 0; long count = 0; };
 
 }  // namespace wm
@@ -233,12 +238,14 @@ struct whisper_state {
     // changed setting never replays a graph captured for another path
     // (gen: g_pdec_gen when a persistent step was captured; its graph holds the stamps pointer and spin limit of
     // that time, so a setter call retires it)
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; bool pdec; int gen; hipGraphExec_t exec; std::vector<KPending> ev; };
+    // pdec: 0 = launch chain, 1 = the persistent step (kernels/pdec.hip), 2 = the batched chain (kernels/bdec.hip)
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; int pdec; int gen; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step
     whisper_state* twin = nullptr;                // second half of a paired batch (full_batch)
     bool pdec_block = false;                      // re-running a step whose persistent launch gave up
+    int step_rows = 0;                            // rows of the decode step being built (all row groups)
     // persistent launches of this state that gave up (a wait timed out: not all 256 workgroups resident, e.g.
     // beside another process's kernels) and were re-run on the per-kernel path; after one, the state's steps
     // take the per-kernel path for kPdecBackoffMs (pdec_off) instead of paying the timeout on every step

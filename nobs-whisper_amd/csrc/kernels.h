@@ -266,6 +266,45 @@ int pdec_cross_splits(int H, int rows);  // key splits per (clip, head): a funct
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st);
 const uint16_t* gelu_table_device();
 
+// ---- batched persistent decoder chain (kernels/bdec.hip) ------------------------------------------------
+// Decode steps of 5..128 clips in the direct cross form: per layer, everything but the pass over the encoder
+// output (xattn_step) runs in one 256-workgroup launch whose phases hand off by row group through counters.
+// Launch (la, lb): the tail of layer la (split merge + Wv, cross-out + residual, LN + FC1 + GELU, FC2 +
+// residual; la = -1: none, the embedding feeds layer 0) then the head of layer lb (LN + QKV with the self-cache
+// append, self attention, out-projection + residual, LN + cross-Q, the Q' projection; lb = L: the final
+// LayerNorm into out_dh instead).
+struct BdecLayer {
+    const void *wqkv, *wo, *wxq, *wxo, *w1, *w2;
+    const void* wv;   // the cross V weights of the layer [d][d] (wkv_cross + (2 l + 1) d^2)
+    const void* wkt;  // the cross K weights per head, transposed [H][d][64]
+    const float *bqkv, *bo, *bxq, *bxo, *b1, *b2, *bv;
+    const float *ln1_w, *ln1_b, *lnx_w, *lnx_b, *ln2_w, *ln2_b;
+};
+struct BdecArgs {
+    const BdecLayer* layers;  // device array [L]
+    int L, M, d, n_text_ctx, S;
+    int la, lb;
+    const void* tok_emb; int te_f32; const float* pos_d;
+    const float *lnd_w, *lnd_b; void* out_dh;
+    const int *tok, *pos, *slot;
+    void* self_cache; float k_scale;
+    float* x;                     // the residual stream [M][d] f32
+    void *bq, *batt, *bff, *bxq;  // q|k|v [M][3d], attention outputs [M][d], GELU rows [M][4d], cross q [M][d] (T)
+    void* qx;                     // Q' [M][2H][d] (T): the E pass's operand
+    const float *opart, *ml;      // the E pass's split partials [M][S][H][d], {m, l} [M][S][H][2]
+    unsigned* cnt;                // hand-off counters + error word (bdec_sync_bytes), zeroed before every step
+    int err_index;                // the error word's index in cnt (bdec_err_index)
+    long spin_ticks;
+    const uint16_t* gelu_tab;
+    int dbg_fence;                // debug (WHISPER_MI355X_BDEC_FENCE): agent release / acquire fences at every hand-off
+    int dbg_head_only;            // debug (WHISPER_MI355X_BDEC_HEAD_ONLY): launches with a layer tail do nothing
+    unsigned long long* stamps;   // debug (g_pdec_stamps): [L + 1 launches][2][9 phases][256 WGs] clock at input / output
+};
+bool bdec_supported(int d);
+size_t bdec_sync_bytes(int L);
+int bdec_err_index(int L);
+void launch_bdec(DType dt, const BdecArgs& a, hipStream_t st);
+
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {
     int n_vocab, eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, space, n_lang;

@@ -43,6 +43,9 @@ SHAPES = {
     "small-4L": (51865, 80, 768, 12, 4, 4),
     "large-v3-2L": (51866, 128, 1280, 20, 2, 2),
     "large-v3-turbo-2L": (51866, 128, 1280, 20, 2, 4),
+    # one encoder and one decoder layer at small's width (kernel debugging: every buffer of a decode step is
+    # the one layer's)
+    "small-1L": (51865, 80, 768, 12, 1, 1),
 }
 
 # "+conf" variant: a decoder whose output distribution is as peaked as a trained model's (random
