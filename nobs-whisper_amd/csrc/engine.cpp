@@ -295,7 +295,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync); dfree(w.bd_sync); dfree(w.bq);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync); dfree(w.bd_sync); dfree(w.bq); dfree(w.bhn);
     if (w.h_pd_err) hipHostFree(w.h_pd_err);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
@@ -382,7 +382,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
         dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.mel_ptrs);
-        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles); dfree(w.bq);
+        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles); dfree(w.bq); dfree(w.bhn);
         for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
             if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
         w.cap_jobs = w.cap_tok = w.cap_cross = w.cap_xq = 0;
@@ -1012,6 +1012,7 @@ static void bdec_prepare(Context* c, whisper_state* s) {
     bdec_layers(c);
     if (!w.bd_sync) dalloc(w.bd_sync, bdec_sync_bytes(c->hp.n_text_layer));
     if (!w.bq) dalloc(w.bq, (size_t)w.cap_jobs * 3 * c->hp.n_text_state * esize(c->dt));
+    if (!w.bhn) dalloc(w.bhn, (size_t)w.cap_jobs * c->hp.n_text_state * esize(c->dt));
     if (!w.h_pd_err) {
         WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
         *w.h_pd_err = 0;
@@ -1026,7 +1027,7 @@ static void decoder_rows_bdec(Context* c, whisper_state* s, const DecView& v, in
     Workspace& w = s->ws;
     const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab, n = v.n, Ta = hp.n_audio_ctx;
     hipStream_t st = v.st;
-    if (!w.bd_sync || !w.bq) WM_FAIL("bdec: buffers not allocated (bdec_prepare)");
+    if (!w.bd_sync || !w.bq || !w.bhn) WM_FAIL("bdec: buffers not allocated (bdec_prepare)");
     const int S = xattn_splits(n, Ta);
     BdecArgs a{};
     a.layers = bdec_layers(c);
@@ -1039,12 +1040,13 @@ static void decoder_rows_bdec(Context* c, whisper_state* s, const DecView& v, in
     a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
     a.self_cache = w.self; a.k_scale = c->k_scale;
     a.x = w.dx + (size_t)v.r0 * d;
-    a.bq = w.bq; a.batt = w.datt; a.bff = w.dff; a.bxq = w.dq; a.qx = w.qx;
+    a.bq = w.bq; a.batt = w.datt; a.bff = w.dff; a.bxq = w.dq; a.qx = w.qx; a.hn = w.bhn;
     a.opart = v.xo; a.ml = v.xml;
     a.cnt = w.bd_sync; a.err_index = bdec_err_index(L);
     a.spin_ticks = g_pdec_spin_ticks;
     a.gelu_tab = gelu_table_device();
     a.dbg_fence = getenv("WHISPER_MI355X_BDEC_FENCE") ? atoi(getenv("WHISPER_MI355X_BDEC_FENCE")) : 0;
+    a.dbg_skip = getenv("WHISPER_MI355X_BDEC_SKIP") ? atoi(getenv("WHISPER_MI355X_BDEC_SKIP")) : 0;
     a.dbg_head_only = getenv("WHISPER_MI355X_BDEC_HEAD_ONLY") ? atoi(getenv("WHISPER_MI355X_BDEC_HEAD_ONLY")) : 0;
     a.stamps = g_pdec_stamps;
     WM_CHECK(hipMemsetAsync(w.bd_sync, 0, bdec_sync_bytes(L), st));

@@ -177,6 +177,7 @@ struct Workspace {
     // batched persistent chain (kernels/bdec.hip): its counters + error word, and the q|k|v rows [cap][3d]
     unsigned* bd_sync = nullptr;
     void* bq = nullptr;
+    void* bhn = nullptr;  // the chain's LayerNorm rows [cap_jobs][d] (T)
     // mel / pcm
     float* pcm = nullptr;
     float* mel = nullptr;

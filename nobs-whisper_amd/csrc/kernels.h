@@ -269,9 +269,9 @@ const uint16_t* gelu_table_device();
 // ---- batched persistent decoder chain (kernels/bdec.hip) ------------------------------------------------
 // Decode steps of 5..128 clips in the direct cross form: per layer, everything but the pass over the encoder
 // output (xattn_step) runs in one 256-workgroup launch whose phases hand off by row group through counters.
-// Launch (la, lb): the tail of layer la (split merge + Wv, cross-out + residual, LN + FC1 + GELU, FC2 +
-// residual; la = -1: none, the embedding feeds layer 0) then the head of layer lb (LN + QKV with the self-cache
-// append, self attention, out-projection + residual, LN + cross-Q, the Q' projection; lb = L: the final
+// Launch (la, lb): the tail of layer la (split merge + Wv, cross-out + residual, LN, FC1 + GELU, FC2 +
+// residual; la = -1: none, the embedding feeds layer 0) then the head of layer lb (LN, QKV with the self-cache
+// append, self attention, out-projection + residual, LN, cross-Q, the Q' projection; lb = L: the final
 // LayerNorm into out_dh instead).
 struct BdecLayer {
     const void *wqkv, *wo, *wxq, *wxo, *w1, *w2;
@@ -291,6 +291,7 @@ struct BdecArgs {
     float* x;                     // the residual stream [M][d] f32
     void *bq, *batt, *bff, *bxq;  // q|k|v [M][3d], attention outputs [M][d], GELU rows [M][4d], cross q [M][d] (T)
     void* qx;                     // Q' [M][2H][d] (T): the E pass's operand
+    void* hn;                     // LayerNorm rows [M][d] (T): the operand of QKV, cross-Q and FC1
     const float *opart, *ml;      // the E pass's split partials [M][S][H][d], {m, l} [M][S][H][2]
     unsigned* cnt;                // hand-off counters + error word (bdec_sync_bytes), zeroed before every step
     int err_index;                // the error word's index in cnt (bdec_err_index)
@@ -298,7 +299,8 @@ struct BdecArgs {
     const uint16_t* gelu_tab;
     int dbg_fence;                // debug (WHISPER_MI355X_BDEC_FENCE): agent release / acquire fences at every hand-off
     int dbg_head_only;            // debug (WHISPER_MI355X_BDEC_HEAD_ONLY): launches with a layer tail do nothing
-    unsigned long long* stamps;   // debug (g_pdec_stamps): [L + 1 launches][2][9 phases][256 WGs] clock at input / output
+    int dbg_skip;                 // debug (WHISPER_MI355X_BDEC_SKIP, timing only): 1 = no weight DMA, 2 = no operand loads
+    unsigned long long* stamps;   // debug (g_pdec_stamps): [L + 1 launches][3][12 phases][256 WGs] clock at input / output / operand
 };
 bool bdec_supported(int d);
 size_t bdec_sync_bytes(int L);

@@ -75,13 +75,11 @@ __device__ __forceinline__ void lput(lchar* base, int off, V v) { *(__attribute_
 constexpr int kG = 256;    // workgroups (one per CU)
 constexpr int kNT = 256;   // threads per workgroup
 constexpr int kRS = 32;    // rows per row group
-constexpr int kNS = 6;     // weight ring stages (64 k each)
 constexpr int kSC1 = 16;   // cache-policy bit of sc1 in the buffer intrinsics' aux operand
-constexpr int kNT_AUX = 2; // non-temporal
 
-enum { PH_T1 = 0, PH_T2, PH_T3, PH_T4, PH_H1, PH_H2, PH_H3, PH_H4, PH_H5, kNPH };
+enum { PH_T1 = 0, PH_T2, PH_T3, PH_T4, PH_T5, PH_H0, PH_H1, PH_H2, PH_H3, PH_H4, PH_H5, PH_H6, kNPH };
 enum { BE_QKV = 0, BE_RESID, BE_SCALE, BE_GELU };
-enum { AS_T = 0, AS_LN, AS_EMB };
+enum { AS_T = 0, AS_LN, AS_EMB };  // a GEMM's operand rows: T rows, LayerNorm of x, LayerNorm of the embedding
 
 __device__ __forceinline__ rsrc_t mkr(const void* p, long bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)std::min<long>(bytes, 0x7fffffffL), 0x00020000);
@@ -126,6 +124,15 @@ __device__ __forceinline__ float sum8(float a) {  // over the 8 lanes of a key r
     a += dppf<0x4E>(a);
     return a + dppf<0x141>(a);
 }
+// a workgroup-uniform value the compiler cannot prove uniform (an argument of a non-inlined callee arrives in a
+// VGPR) moved to an SGPR
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+template <class P>
+__device__ __forceinline__ P* uni(P* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((unsigned)v), hi = (uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (P*)(lo | (hi << 32));
+}
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // s_waitcnt vmcnt(n) for a run-time n (the immediate must be a constant)
@@ -134,9 +141,23 @@ __device__ __forceinline__ void vm_wait(int n) {
 #define WM_VW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
         WM_VW(0) WM_VW(1) WM_VW(2) WM_VW(3) WM_VW(4) WM_VW(5) WM_VW(6) WM_VW(7) WM_VW(8) WM_VW(9) WM_VW(10)
         WM_VW(11) WM_VW(12) WM_VW(13) WM_VW(14) WM_VW(15) WM_VW(16) WM_VW(17) WM_VW(18) WM_VW(19) WM_VW(20)
+        WM_VW(21) WM_VW(22) WM_VW(23) WM_VW(24) WM_VW(25) WM_VW(26) WM_VW(27) WM_VW(28) WM_VW(29) WM_VW(30)
+        WM_VW(31) WM_VW(32) WM_VW(33) WM_VW(34) WM_VW(35) WM_VW(36) WM_VW(37) WM_VW(38) WM_VW(39) WM_VW(40)
+        WM_VW(41) WM_VW(42) WM_VW(43) WM_VW(44) WM_VW(45) WM_VW(46) WM_VW(47) WM_VW(48) WM_VW(49) WM_VW(50)
+        WM_VW(51) WM_VW(52) WM_VW(53) WM_VW(54) WM_VW(55) WM_VW(56) WM_VW(57) WM_VW(58) WM_VW(59) WM_VW(60)
+        WM_VW(61) WM_VW(62) WM_VW(63)
 #undef WM_VW
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
+}
+// s_waitcnt vmcnt(2 n) for n ring steps of two DMA instructions still allowed in flight, n in [0, NS - 2]
+template <int NS>
+__device__ __forceinline__ void vm_wait_steps(int n) {
+    if (n >= NS - 2) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NS - 2)) : "memory");
+        return;
+    }
+    vm_wait(2 * n);
 }
 template <typename T>
 __device__ __forceinline__ u32x2 pack4(const float (&v)[4]) {
@@ -158,8 +179,10 @@ struct BG {
     static constexpr int CPR = D / 8;                 // 16-byte chunks per operand row (a super-chunk of K = D)
     static constexpr int A_BYTES = kRS * D * 2;       // operand image [32][D] T
     static constexpr int MAXCT = (D + 255) / 256;     // column tiles per worker at WPR = 64 (FC1: 4D / 16 / 64)
-    static constexpr int STAGE = MAXCT * 16 * 128;    // one ring stage: MAXCT x 16 weight rows x 64 k
-    static constexpr int RING = kNS * STAGE;
+    // one wave's weight ring: a quarter of the rest of the 160 KB, in 1-KB slots (one MFMA fragment each)
+    static constexpr int RW = ((160 * 1024 - A_BYTES - 1024) / 4) & ~1023;
+    static constexpr int NS = RW / 2048 < 32 ? RW / 2048 : 32;  // its slots of 16 weight rows x 64 k
+    static constexpr int RING = 4 * RW;
     static constexpr int LDS = A_BYTES + RING + 64;
 };
 
@@ -169,10 +192,19 @@ template <int D>
 __device__ __forceinline__ int a_off(int row, int ch) {
     return row * D * 2 + (((ch & ~15) | ((ch & 15) ^ (row & 15))) << 4);
 }
-// weight ring stage: [nct x 16 rows][8 chunks] (128 bytes per row), chunk swizzle (row >> 1) & 7
-__device__ __forceinline__ int w_off(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
 }  // namespace
+
+// A phase's copy of the context's coordinates: a member read through `this` is a flat load of the stack object
+// whenever the callee is not inlined, and the compiler then waits vmcnt(0) for it, draining the weight ring
+// (the workgroup-uniform ones through readfirstlane, so that loop counters and the counted waits stay scalar)
+#define BD_LOCALS                                                                                            \
+    const int lane = this->lane, tid = this->tid;                                                             \
+    const int wave = __builtin_amdgcn_readfirstlane(this->wave), r0 = __builtin_amdgcn_readfirstlane(this->r0); \
+    const int cw = __builtin_amdgcn_readfirstlane(this->cw), wpr = __builtin_amdgcn_readfirstlane(this->wpr);   \
+    lchar* const lds = this->lds;                                                                            \
+    CArgs& a = this->a;                                                                                      \
+    (void)lane; (void)wave; (void)tid; (void)r0; (void)cw; (void)wpr; (void)lds
 
 // The launch's arguments read in place from the kernarg segment (constant address space: scalar loads). A
 // reference to the by-value kernel parameter would make hipcc copy the whole struct to scratch first.
@@ -195,7 +227,7 @@ struct BdecCtx {
     __device__ BdecCtx(CArgs& a_, lchar* l) : a(a_), lds(l) {
         w = blockIdx.x;
         tid = ptid();
-        wave = tid >> 6;
+        wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         lane = tid & 63;
         nrg = (a.M + kRS - 1) / kRS;
         lg = nrg <= 1 ? 0 : nrg <= 2 ? 1 : 2;
@@ -225,10 +257,11 @@ struct BdecCtx {
         }
         if (tid == 0) __hip_atomic_fetch_add(counter(layer, ph, rg, w & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // debug timeline (tools/bdec_stamps.py): the 100 MHz clock when phase ph's input arrived (k = 0) / its output
-    // was published (k = 1), per launch and workgroup (a vector store from lane 0)
+    // debug timeline (tools/bdec_stamps.py): the 100 MHz clock when phase ph's input arrived (k = 0), its output
+    // was published (k = 1), its first operand image was in LDS (k = 2, GEMM phases), per launch and workgroup
+    // (a vector store from lane 0)
     __device__ void stamp(int ph, int k) const {
-        if (a.stamps && tid == 0) a.stamps[(((long)(a.la + 1) * 2 + k) * kNPH + ph) * kG + w] = __builtin_amdgcn_s_memrealtime();
+        if (a.stamps && tid == 0) a.stamps[(((long)(a.la + 1) * 3 + k) * kNPH + ph) * kG + w] = __builtin_amdgcn_s_memrealtime();
     }
     // wait until every worker of this row group arrived at (layer, ph); false = give up (the caller returns)
     __device__ bool wait(int layer, int ph) {
@@ -271,6 +304,7 @@ struct BdecCtx {
     // ---- operand loading into the image ------------------------------------------------------------
     // rows r0.. r0+31 of a T matrix [M][ld] (handed off: sc1 loads), columns [k0, k0 + D)
     __device__ void load_a_t(const T* src, int ld, int k0) {
+        BD_LOCALS;
         const rsrc_t r = mkr(src, (long)a.M * ld * 2);  // rows >= M read 0
         constexpr int CPR = BG<D>::CPR, NCH = kRS * CPR / kNT;
         u32x4 v[NCH];
@@ -285,14 +319,13 @@ struct BdecCtx {
             lput<u32x4>(lds, a_off<D>(row, c), v[u]);
         }
     }
-    // LayerNorm rows (ggml_norm: double sums, float mean / variance, (v * scale) * w + b separately rounded)
-    // of the f32 residual x (sc1 loads) or of the token + position embedding (emb), into the image (to_lds) or
-    // to global rows of `gout` [M][D] T. Wave q normalises rows 8q .. 8q + 7; lane l holds columns
-    // 4 l + 256 e (+ 0..3), summed in e, then j order, then over the lanes by the fixed DPP tree.
-    __device__ void load_a_ln(const float* x, bool emb, const float* gw, const float* gb, bool to_lds, T* gout) {
+    // ---- operand image from LayerNorm rows: wave q normalises rows 8 q .. 8 q + 7 of the f32 residual x (sc1
+    // loads; a batch of rows' loads in flight together) or of the token + position embedding (emb), ggml_norm's
+    // arithmetic as ln_phase's, and writes them rounded to T into the image
+    __device__ void load_a_ln(const float* x, bool emb, const float* gw, const float* gb) {
 #pragma clang fp contract(off)
-        constexpr int NE = D / 256;
-        const rsrc_t rx = mkr(x, (long)a.M * D * 4);
+        BD_LOCALS;
+        constexpr int NE = D / 256, RB = NE <= 3 ? 4 : 2;
         float g[NE][4], b[NE][4];
 #pragma unroll
         for (int e = 0; e < NE; e++) {
@@ -301,30 +334,135 @@ struct BdecCtx {
             g[e][0] = gv.x; g[e][1] = gv.y; g[e][2] = gv.z; g[e][3] = gv.w;
             b[e][0] = bv.x; b[e][1] = bv.y; b[e][2] = bv.z; b[e][3] = bv.w;
         }
-        const T* te = (const T*)a.tok_emb;
-        const float* te32 = (const float*)a.tok_emb;
-#pragma unroll 1
-        for (int rr = 0; rr < 8; rr++) {
-            const int row = wave * 8 + rr, m = r0 + row;
-            float v[NE][4];
+        const rsrc_t rx = mkr(x, (long)a.M * D * 4);
+#pragma unroll
+        for (int r8 = 0; r8 < 8; r8 += RB) {
+            float v[RB][NE][4];
             if (emb) {
-                const int mm = m < a.M ? m : 0;
-                const long t = a.tok[mm], p = a.pos[mm];
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++) {
+                    const int m0 = r0 + wave * 8 + r8 + rr, m = m0 < a.M ? m0 : 0;
+                    const long t = a.tok[m], p = a.pos[m];
+#pragma unroll
+                    for (int e = 0; e < NE; e++) {
+                        const int k = 4 * lane + 256 * e;
+                        const float4 pv = *(const float4*)(a.pos_d + p * D + k);
+                        float tv[4];
+                        if (a.te_f32) {
+                            const float4 q = *(const float4*)((const float*)a.tok_emb + t * D + k);
+                            tv[0] = q.x; tv[1] = q.y; tv[2] = q.z; tv[3] = q.w;
+                        } else {
+                            const u32x2 q = *(const u32x2*)((const T*)a.tok_emb + t * D + k);
+                            const T* qe = (const T*)&q;
+#pragma unroll
+                            for (int j = 0; j < 4; j++) tv[j] = (float)qe[j];
+                        }
+                        v[rr][e][0] = tv[0] + pv.x; v[rr][e][1] = tv[1] + pv.y; v[rr][e][2] = tv[2] + pv.z; v[rr][e][3] = tv[3] + pv.w;
+                    }
+                }
+            } else {
+                u32x4 q[RB][NE];
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++)
+#pragma unroll
+                    for (int e = 0; e < NE; e++)
+                        q[rr][e] = ld16(rx, (uint32_t)(((long)(r0 + wave * 8 + r8 + rr) * D + 4 * lane + 256 * e) * 4));
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++)
+#pragma unroll
+                    for (int e = 0; e < NE; e++) {
+                        // (whole-vector cast: an element-wise cast of a buffer load's lanes lets this compiler narrow the
+                        // load to its first dword and broadcast it, see DESIGN.md "toolchain notes")
+                        const f32x4 f = __builtin_bit_cast(f32x4, q[rr][e]);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) v[rr][e][j] = f[j];
+                    }
+            }
+#pragma unroll
+            for (int rr = 0; rr < RB; rr++) {
+                double s = 0.0;
+#pragma unroll
+                for (int e = 0; e < NE; e++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) s += (double)v[rr][e][j];
+                s = wave_sum_d(s);
+                const float mean = (float)(s / D);
+                double s2 = 0.0;
+#pragma unroll
+                for (int e = 0; e < NE; e++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        v[rr][e][j] = v[rr][e][j] - mean;
+                        s2 += (double)(v[rr][e][j] * v[rr][e][j]);
+                    }
+                s2 = wave_sum_d(s2);
+                const float variance = (float)(s2 / D);
+                const float scale = 1.0f / sqrtf(variance + 1e-5f);
+                const int row = wave * 8 + r8 + rr;
+#pragma unroll
+                for (int e = 0; e < NE; e++) {
+                    float y[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        float t = v[rr][e][j] * scale;
+                        t = t * g[e][j];
+                        y[j] = t + b[e][j];
+                    }
+                    const int k = 4 * lane + 256 * e;
+                    lput<u32x2>(lds, a_off<D>(row, k >> 3) + ((k >> 2) & 1) * 8, pack4<T>(y));
+                }
+            }
+        }
+    }
+
+    // ---- LayerNorm phase (the final LayerNorm): row r0 + cw of the row group (workers cw < 32, wave 0) ------
+    // ggml_norm: double sums, float mean / variance, (v * scale) * w + b separately rounded; lane l holds columns
+    // 4 l + 256 e (+ 0..3), summed in e, then j order, then over the lanes by the fixed DPP tree. Input: the f32
+    // residual x (sc1 loads) or, for layer 0's head (emb), the token + position embedding, which also becomes
+    // x. Output: the row rounded to T (sc1 stores), the next GEMM's operand.
+    __device__ bool ln_phase(int layer, int ph, int wait_layer, int wait_ph, bool emb, const float* gw, const float* gb,
+                             T* out) {
+#pragma clang fp contract(off)
+        BD_LOCALS;
+        constexpr int NE = D / 256;
+        const int m = r0 + cw;
+        const bool row = cw < kRS && m < a.M;  // (workgroup-uniform)
+        float g[NE][4], b[NE][4];
+        if (row && wave == 0) {  // the parameters before the wait
+#pragma unroll
+            for (int e = 0; e < NE; e++) {
+                const float4 gv = *(const float4*)(gw + 4 * lane + 256 * e);
+                const float4 bv = *(const float4*)(gb + 4 * lane + 256 * e);
+                g[e][0] = gv.x; g[e][1] = gv.y; g[e][2] = gv.z; g[e][3] = gv.w;
+                b[e][0] = bv.x; b[e][1] = bv.y; b[e][2] = bv.z; b[e][3] = bv.w;
+            }
+        }
+        if (row && wait_ph >= 0 && !wait(wait_layer, wait_ph)) return false;
+        stamp(ph, 0);
+        if (row && wave == 0) {
+            float v[NE][4];
+            const rsrc_t rx = mkr(a.x, (long)a.M * D * 4);
+            if (emb) {
+                const long t = a.tok[m], p = a.pos[m];
 #pragma unroll
                 for (int e = 0; e < NE; e++) {
                     const int k = 4 * lane + 256 * e;
                     const float4 pv = *(const float4*)(a.pos_d + p * D + k);
                     float tv[4];
                     if (a.te_f32) {
-                        const float4 q = *(const float4*)(te32 + t * D + k);
+                        const float4 q = *(const float4*)((const float*)a.tok_emb + t * D + k);
                         tv[0] = q.x; tv[1] = q.y; tv[2] = q.z; tv[3] = q.w;
                     } else {
-                        const u32x2 q = *(const u32x2*)(te + t * D + k);
+                        const u32x2 q = *(const u32x2*)((const T*)a.tok_emb + t * D + k);
                         const T* qe = (const T*)&q;
 #pragma unroll
                         for (int j = 0; j < 4; j++) tv[j] = (float)qe[j];
                     }
                     v[e][0] = tv[0] + pv.x; v[e][1] = tv[1] + pv.y; v[e][2] = tv[2] + pv.z; v[e][3] = tv[3] + pv.w;
+                    u32x4 o;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) o[j] = __builtin_bit_cast(uint32_t, v[e][j]);
+                    st16(rx, (uint32_t)(((long)m * D + k) * 4), o);  // x = the embedding (the residual of H3)
                 }
             } else {
                 u32x4 q[NE];
@@ -357,6 +495,7 @@ struct BdecCtx {
             s2 = wave_sum_d(s2);
             const float variance = (float)(s2 / D);
             const float scale = 1.0f / sqrtf(variance + 1e-5f);
+            const rsrc_t ro = mkr(out, (long)a.M * D * 2);
 #pragma unroll
             for (int e = 0; e < NE; e++) {
                 float y[4];
@@ -366,120 +505,144 @@ struct BdecCtx {
                     t = t * g[e][j];
                     y[j] = t + b[e][j];
                 }
-                const u32x2 pk = pack4<T>(y);
-                const int k = 4 * lane + 256 * e;
-                if (to_lds) {
-                    lput<u32x2>(lds, a_off<D>(row, k >> 3) + ((k >> 2) & 1) * 8, pk);
-                } else if (m < a.M) {
-                    *(u32x2*)(gout + (long)m * D + k) = pk;
-                }
+                st8(ro, (uint32_t)(((long)m * D + 4 * lane + 256 * e) * 2), pack4<T>(y));
             }
         }
+        arrive(layer, ph);
+        stamp(ph, 1);
+        return true;
     }
 
-    // ---- a GEMM phase: rows r0.. +31, this worker's 16-column tiles of W [N][K] over the whole K ------------
+    // ---- a GEMM phase: rows r0 .. r0 + 31, this worker's 16-column tiles of W [N][K] over the whole K ----------
+    // The operand rows A [M][K] (T, handed off) go into the LDS image one super-chunk of D columns at a time
+    // (FC2: four). The weights stream through wave-private rings by LDS-DMA, a slot = 16 weight rows x 64 k
+    // (two DMA instructions of 8 whole 128-byte lines; chunks XOR-swizzled by (row >> 1) & 7), so a wave waits
+    // only for its own DMA (counted vmcnt) and never for the other waves: no barrier per k-step. The weights use
+    // the default cache policy: the row groups' workers with equal blockIdx % 8 share an XCD and read the same
+    // columns. Wave q takes the 64-k steps q, q + 4, ... of every super-chunk, tile after tile, and sums them
+    // into f32 accumulators; the four waves' partials are added in wave order through LDS at the end, then bias
+    // and the epilogue. The summation order depends on K and the tile only, not on M or the other rows.
     template <int EPI, int ASRC>
     __device__ bool gemm(int layer, int ph, int wait_layer, int wait_ph, const T* W, const float* bias, int N, int K,
-                         const T* asrc, const float* gw, const float* gb, void* out, int ldo) {
-        lchar* ring = lds + BG<D>::A_BYTES;
+                         const void* A, void* out, int ldo, const float* gw = nullptr, const float* gb = nullptr) {
+        BD_LOCALS;
+        layer = uni(layer); N = uni(N); K = uni(K); ldo = uni(ldo);
+        W = uni(W); A = uni(A); out = uni(out);
+        constexpr int MAXCT = BG<D>::MAXCT, NKI = D / 256;  // a wave's 64-k steps per super-chunk
+        constexpr int NS = BG<D>::NS;                          // ring slots
+        constexpr int NI = (2 * MAXCT * 64 + kNT - 1) / kNT;   // epilogue items per thread
         const int nct_all = N / 16;
         const int ct0 = (int)((long)cw * nct_all / wpr), nct = (int)((long)(cw + 1) * nct_all / wpr) - ct0;
-        const int nst = K / 64;
-        const int np = nct * 2;                        // 8-row DMA pieces per stage
-        const int ppw = (np + 3) >> 2;                 // pieces per wave per stage (the last piece repeated)
-        const int rowW0 = ct0 * 16;
-        auto issue = [&](int st) {
-            lchar* dst = ring + (st % kNS) * BG<D>::STAGE;
-            for (int i = 0; i < ppw; i++) {
-                const int p = min(wave + 4 * i, np - 1);
-                const int r = p * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-                const T* src = W + (long)(rowW0 + r) * K + st * 64 + c * 8;
-                __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + p * 1024), 16, 0, kNT_AUX);
+        const int nsc = K / D;
+        const int nstep = nsc * NKI * nct;  // the wave's stream: step (j, t) = j * nct + t, j = its 64-k steps
+        const bool skip_w = (a.dbg_skip & 1) != 0, skip_a = (a.dbg_skip & 2) != 0;
+        lchar* ring = lds + BG<D>::A_BYTES + wave * BG<D>::RW;
+        // DMA lane: row wr (+ 8 in the second instruction) of the slot, the chunk that lands at its position
+        const int wr = lane >> 3, wc0 = (lane & 7) ^ ((wr >> 1) & 7), wc1 = (lane & 7) ^ (((wr + 8) >> 1) & 7);
+        const T* wl = W + (long)(ct0 * 16 + wr) * K + wc0 * 8 + wave * 64;
+        const long wl1 = 8L * K + (wc1 - wc0) * 8;  // the second instruction's source, relative
+        // the next step to issue: (ij, it) into slot islot
+        int ij = 0, it = 0, islot = 0, nissued = 0;
+        auto issue = [&]() {
+            if (!skip_w) {
+                const T* src = wl + (long)it * 16 * K + (long)ij * 256;
+                lchar* dst = ring + islot * 2048;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)dst, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(src + wl1), (lds_ptr_t)(dst + 1024), 16, 0, 0);
+            }
+            nissued++;
+            islot = islot == NS - 1 ? 0 : islot + 1;
+            if (++it == nct) {
+                it = 0;
+                ij++;
             }
         };
-        const int npre = nct > 0 ? min(nst, kNS - 1) : 0;
-        for (int st = 0; st < npre; st++) issue(st);
-        // the residual this worker updates (its own tiles, written by its previous residual phase)
-        const int rt = wave & 1, jh = wave >> 1;
-        const int jn = (nct + 1) >> 1, j0 = jh ? jn : 0, j1 = jh ? nct : jn;
-        constexpr int MJ = (BG<D>::MAXCT + 1) / 2;
-        const int mrow = r0 + rt * 16 + (lane & 15);
-        u32x4 xold[MJ];
-        if constexpr (EPI == BE_RESID) {
-            const rsrc_t rx = mkr(out, (long)a.M * ldo * 4);
-#pragma unroll
-            for (int j = 0; j < MJ; j++) {
-                const int n = (ct0 + j0 + j) * 16 + 4 * (lane >> 4);
-                const bool use = j0 + j < j1 && !(a.la < 0 && a.lb == 0);  // (the embedding case computes it later)
-                xold[j] = use ? ld16(rx, (uint32_t)(((long)mrow * ldo + n) * 4)) : u32x4{0, 0, 0, 0};
-            }
-        }
+        // a fragment lane's byte offset in a slot: row lane & 15, chunk 4 s + (lane >> 4) of sub-step s
+        const int fr = lane & 15, fo0 = fr * 128 + (((lane >> 4) ^ ((fr >> 1) & 7)) << 4),
+                  fo1 = fr * 128 + (((4 + (lane >> 4)) ^ ((fr >> 1) & 7)) << 4);
+        const int npre = min(nstep, NS - 1);
+        for (int g = 0; g < npre; g++) issue();
         // (a worker without column tiles reads nothing: it arrives without waiting)
         if (nct > 0 && wait_ph >= 0 && !wait(wait_layer, wait_ph)) return false;
         stamp(ph, 0);
-        f32x4 acc[MJ];
-#pragma unroll
-        for (int j = 0; j < MJ; j++) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int nsc = K / D;
         if (nct > 0) {
+            const int nit = 2 * nct * 64;
+            u32x4 xold[NI];
+            if constexpr (EPI == BE_RESID) {  // the residual this worker updates (loaded behind the wait)
+                const rsrc_t rx = mkr(out, (long)a.M * ldo * 4);
+#pragma unroll
+                for (int u = 0; u < NI; u++) {
+                    const int i = tid + kNT * u, rt = i / (nct * 64), rem = i - rt * nct * 64, t = rem >> 6, l = rem & 63;
+                    const int n = (ct0 + t) * 16 + 4 * (l >> 4), mrow = r0 + rt * 16 + (l & 15);
+                    xold[u] = i < nit ? ld16(rx, (uint32_t)(((long)mrow * ldo + n) * 4)) : u32x4{0, 0, 0, 0};
+                }
+            }
+            f32x4 acc[2][MAXCT];
+#pragma unroll
+            for (int t = 0; t < MAXCT; t++) acc[0][t] = acc[1][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            int g = 0, slot = 0;
             for (int sc = 0; sc < nsc; sc++) {
                 if (sc > 0) lds_barrier();  // every wave is done with the previous image
-                if constexpr (ASRC == AS_T) load_a_t(asrc, K, sc * D);
-                else load_a_ln((const float*)asrc, ASRC == AS_EMB, gw, gb, true, nullptr);
-                vm_wait_all();  // (also retires the ring stages issued so far)
-                lds_barrier();
-                if (a.dbg_head_only == 2 && ph == PH_H4 && ct0 == 0) {  // debug: H4's operand image -> bq rows
-                    constexpr int CPR = BG<D>::CPR;
-                    for (int i = tid; i < kRS * CPR; i += kNT) {
-                        const int row = i / CPR, c = i - row * CPR;
-                        *(u32x4*)((T*)a.bq + ((long)(r0 + row) * D + c * 8)) = lget<u32x4>(lds, a_off<D>(row, c));
-                    }
+                if (skip_a) {
+                } else if constexpr (ASRC == AS_T) {
+                    load_a_t((const T*)A, K, sc * D);
+                } else {
+                    load_a_ln((const float*)A, ASRC == AS_EMB, gw, gb);
                 }
-                const int st_lo = sc * (D / 64), st_hi = st_lo + D / 64;
-                for (int st = st_lo; st < st_hi; st++) {
-                    // stages issued before this one's wait: min(nst, st + kNS - 1) (a super-chunk start drained them)
-                    const int issued = min(nst, st + kNS - 1);
-                    if (st > st_lo) {
-                        vm_wait(ppw * (issued - st - 1));
-                        lds_barrier();
-                    }
-                    if (st + kNS - 1 < nst) issue(st + kNS - 1);
-                    const lchar* sl = ring + (st % kNS) * BG<D>::STAGE;
-                    const int kk0 = (st - st_lo) * 2;
+                vm_wait_all();  // (also retires the weight steps issued so far)
+                lds_barrier();
+                if (sc == 0) stamp(ph, 2);
+                for (int jj = 0; jj < NKI; jj++) {
+                    // the operand fragments of this 64-k step, shared by the tiles
+                    const int ch = (4 * jj + wave) * 8 + (lane >> 4);
+                    const FT a00 = lget<FT>(lds, a_off<D>(lane & 15, ch)), a01 = lget<FT>(lds, a_off<D>(lane & 15, ch + 4));
+                    const FT a10 = lget<FT>(lds, a_off<D>(16 + (lane & 15), ch)), a11 = lget<FT>(lds, a_off<D>(16 + (lane & 15), ch + 4));
 #pragma unroll
-                    for (int ks = 0; ks < 2; ks++) {
-                        const FT af = lget<FT>(lds, a_off<D>(rt * 16 + (lane & 15), (kk0 + ks) * 4 + (lane >> 4)));
-#pragma unroll
-                        for (int j = 0; j < MJ; j++) {
-                            if (j0 + j < j1) {  // (wave-uniform)
-                                const FT bf = lget<FT>(sl, w_off((j0 + j) * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-                                acc[j] = mfma16x16x32(bf, af, acc[j]);
-                            }
-                        }
+                    for (int t = 0; t < MAXCT; t++) {
+                        if (t >= nct) break;
+                        // step g landed: at most the steps issued after it still in flight
+                        vm_wait_steps<NS>(nissued - g - 1);
+                        const lchar* sl = ring + slot * 2048;
+                        const FT b0 = lget<FT>(sl, fo0), b1 = lget<FT>(sl, fo1);
+                        if (nissued < nstep) issue();  // into the slot read one step ago
+                        acc[0][t] = mfma16x16x32(b0, a00, acc[0][t]);
+                        acc[1][t] = mfma16x16x32(b0, a10, acc[1][t]);
+                        acc[0][t] = mfma16x16x32(b1, a01, acc[0][t]);
+                        acc[1][t] = mfma16x16x32(b1, a11, acc[1][t]);
+                        g++;
+                        slot = slot == NS - 1 ? 0 : slot + 1;
                     }
                 }
             }
-        }
-        // epilogue: lane holds columns n .. n + 3 of row mrow
-        if (mrow < a.M) {
+            // the waves' partials -> LDS [wave][rt][t][lane], summed in wave order
+            lds_barrier();
+            lchar* red = lds + BG<D>::A_BYTES;
 #pragma unroll
-            for (int j = 0; j < MJ; j++) {
-                if (j0 + j >= j1) continue;
-                const int n = (ct0 + j0 + j) * 16 + 4 * (lane >> 4);
+            for (int t = 0; t < MAXCT; t++) {
+                if (t >= nct) break;
+#pragma unroll
+                for (int rt = 0; rt < 2; rt++) lput<f32x4>(red, (((wave * 2 + rt) * MAXCT + t) * 64 + lane) * 16, acc[rt][t]);
+            }
+            lds_barrier();
+            // epilogue: item (rt, t, l) holds columns n .. n + 3 of row mrow
+#pragma unroll
+            for (int u = 0; u < NI; u++) {
+                const int i = tid + kNT * u, rt = i / (nct * 64), rem = i - rt * nct * 64, t = rem >> 6, l = rem & 63;
+                const int n = (ct0 + t) * 16 + 4 * (l >> 4), mrow = r0 + rt * 16 + (l & 15);
+                if (i >= nit || mrow >= a.M) continue;
+                f32x4 sum = lget<f32x4>(red, ((rt * MAXCT + t) * 64 + l) * 16);
+#pragma unroll
+                for (int q = 1; q < 4; q++) sum += lget<f32x4>(red, (((q * 2 + rt) * MAXCT + t) * 64 + l) * 16);
                 const float4 bb = bias ? *(const float4*)(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-                float v[4] = {acc[j][0] + bb.x, acc[j][1] + bb.y, acc[j][2] + bb.z, acc[j][3] + bb.w};
+                float v[4] = {sum[0] + bb.x, sum[1] + bb.y, sum[2] + bb.z, sum[3] + bb.w};
                 if constexpr (EPI == BE_RESID) {
-                    float xo[4];
-                    if (a.la < 0 && a.lb == 0) {  // layer 0's head launch: x = the embedding
-                        const long t = a.tok[mrow], p = a.pos[mrow];
+                    f32x4 xo = __builtin_bit_cast(f32x4, xold[u]);  // (whole-vector cast, as in load_a_ln)
+                    if (a.la < 0 && a.lb == 0) {  // layer 0's head launch: the residual is the embedding
+                        const long tk = a.tok[mrow], p = a.pos[mrow];
 #pragma unroll
                         for (int r = 0; r < 4; r++)
-                            xo[r] = (a.te_f32 ? ((const float*)a.tok_emb)[t * D + n + r] : (float)((const T*)a.tok_emb)[t * D + n + r]) +
+                            xo[r] = (a.te_f32 ? ((const float*)a.tok_emb)[tk * D + n + r] : (float)((const T*)a.tok_emb)[tk * D + n + r]) +
                                     a.pos_d[p * D + n + r];
-                    } else {
-                        const f32x4 f = __builtin_bit_cast(f32x4, xold[j]);  // (whole-vector cast, as in load_a_ln)
-#pragma unroll
-                        for (int r = 0; r < 4; r++) xo[r] = f[r];
                     }
                     u32x4 o;
 #pragma unroll
@@ -517,6 +680,7 @@ struct BdecCtx {
 
     // ---- T1: merge the cross-attention splits of (row group, head h, half b of the rows) and apply Wv -------
     __device__ bool combine(int layer, CLayer& Lw) {
+        BD_LOCALS;
         const int S = a.S;
         const int j = cw, h = j >> 1, half = j & 1;
         const bool task = j < 2 * H;
@@ -540,6 +704,45 @@ struct BdecCtx {
                     for (int s = 0; s < S; s++) wgt[tid * 16 + s] = 0.0f;
                 }
             }
+            __syncthreads();
+            // merged E~ = sum_s w_s O_s (f32), split into hi + lo rows of the image (rows 0-15 hi, 16-31 lo); a
+            // split's loads of every element of the thread are in flight together (one latency per split)
+            constexpr int Q4 = D / 4, NE = 16 * Q4 / kNT;
+            {
+                f32x4 mg[NE];
+#pragma unroll
+                for (int u = 0; u < NE; u++) mg[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                for (int s = 0; s < S; s++) {
+                    f32x4 xv[NE];
+#pragma unroll
+                    for (int u = 0; u < NE; u++) {
+                        const int e = tid + kNT * u, t = e / Q4, c = (e - t * Q4) * 4;
+                        const int m = min(mb + t, a.M - 1);
+                        xv[u] = __builtin_nontemporal_load((const f32x4*)(a.opart + (((long)m * S + s) * H + h) * D + c));
+                    }
+#pragma unroll
+                    for (int u = 0; u < NE; u++) {
+                        const int t = (tid + kNT * u) / Q4;
+                        const float wt = wgt[t * 16 + s];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) mg[u][k] += wt * xv[u][k];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < NE; u++) {
+                    const int e = tid + kNT * u, t = e / Q4, c = (e - t * Q4) * 4;
+                    float hi[4], lo[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const T th = (T)mg[u][k];
+                        hi[k] = (float)th;
+                        lo[k] = mg[u][k] - hi[k];
+                    }
+                    const int ch = c >> 3, hf = ((c >> 2) & 1) * 8;
+                    lput<u32x2>(lds, a_off<D>(t, ch) + hf, pack4<T>(hi));
+                    lput<u32x2>(lds, a_off<D>(16 + t, ch) + hf, pack4<T>(lo));
+                }
+            }
             // Wv fragments of this wave's k-steps (ks = wave + 4 u), 4 column tiles (the head's 64 outputs)
             const T* wv = (const T*)Lw.wv;
             FT wf[KW][4];
@@ -548,31 +751,6 @@ struct BdecCtx {
 #pragma unroll
                 for (int c = 0; c < 4; c++)
                     wf[u][c] = *(const FT*)(wv + ((long)h * 64 + c * 16 + (lane & 15)) * D + (wave + 4 * u) * 32 + 8 * (lane >> 4));
-            __syncthreads();
-            // merged E~ = sum_s w_s O_s (f32), split into hi + lo rows of the image (rows 0-15 hi, 16-31 lo)
-            constexpr int Q4 = D / 4, NE = 16 * Q4 / kNT;
-#pragma unroll 1
-            for (int u = 0; u < NE; u++) {
-                const int e = tid + kNT * u, t = e / Q4, c = (e - t * Q4) * 4;
-                const int m = min(mb + t, a.M - 1);
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int s = 0; s < S; s++) {
-                    const f32x4 x = __builtin_nontemporal_load((const f32x4*)(a.opart + (((long)m * S + s) * H + h) * D + c));
-                    const float wt = wgt[t * 16 + s];
-                    acc.x += wt * x[0]; acc.y += wt * x[1]; acc.z += wt * x[2]; acc.w += wt * x[3];
-                }
-                const float vv[4] = {acc.x, acc.y, acc.z, acc.w};
-                float hi[4], lo[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const T th = (T)vv[k];
-                    hi[k] = (float)th;
-                    lo[k] = vv[k] - hi[k];
-                }
-                const int ch = c >> 3, hf = ((c >> 2) & 1) * 8;
-                lput<u32x2>(lds, a_off<D>(t, ch) + hf, pack4<T>(hi));
-                lput<u32x2>(lds, a_off<D>(16 + t, ch) + hf, pack4<T>(lo));
-            }
             __syncthreads();
             f32x4 acc[2][4];
 #pragma unroll
@@ -615,23 +793,46 @@ struct BdecCtx {
     }
 
     // ---- H2: self attention, one wave per (clip, head) task (attn_self_step_kernel's arithmetic) ----------
+    // A task's first 64 cached keys and values (earlier steps' rows: not handed off) are issued with its q / k /
+    // v loads, one round trip per task; the wave's first task's before the hand-off wait.
     __device__ bool self_attn(int layer) {
+        BD_LOCALS;
+        constexpr int U = 8;
+        const u32x4 zero = {0, 0, 0, 0};
+        const int lane8 = lane & 7, grp = lane >> 3;
+        const T* cache = (const T*)a.self_cache;
+        const int t_first = cw * 4 + wave, t_step = wpr * 4;
+        u32x4 rk[U], rv[U];
+        auto kv_first = [&](int t) {
+            const int m = r0 + t / H, h = t % H;
+            const bool ok = t < kRS * H && m < a.M;
+            const int pos = ok ? a.pos[m] : 0;
+            const long sl = ok ? a.slot[m] : 0;
+            const T* K = cache + (((sl * a.L + layer) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
+            const T* V = cache + (((sl * a.L + layer) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int tt = grp + 8 * u;
+                rk[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(K + (long)tt * 64 + lane8 * 8)) : zero;
+                rv[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(V + (long)tt * 64 + lane8 * 8)) : zero;
+            }
+        };
+        kv_first(t_first);
         if (!wait(layer, PH_H1)) return false;
         stamp(PH_H2, 0);
         lfloat* qs = (lfloat*)lds + wave * (3 * 64 + 448);
         lfloat* ks = qs + 64;
         lfloat* vs = qs + 128;
         lfloat* sc = qs + 192;
-        const int lane8 = lane & 7, grp = lane >> 3;
-        const T* cache = (const T*)a.self_cache;
         const rsrc_t rq = mkr(a.bq, (long)a.M * 3 * D * 2);
-        for (int t = cw * 4 + wave; t < kRS * H; t += wpr * 4) {
+        for (int t = t_first; t < kRS * H; t += t_step) {
             const int m = r0 + t / H, h = t % H;
             if (m >= a.M) break;  // (wave-uniform; tasks are in row order)
             const int pos = a.pos[m];
             const long sl = a.slot[m];
             const T* K = cache + (((sl * a.L + layer) * 2 + 0) * H + h) * (long)a.n_text_ctx * 64;
             const T* V = cache + (((sl * a.L + layer) * 2 + 1) * H + h) * (long)a.n_text_ctx * 64;
+            if (t != t_first) kv_first(t);
             // q, k, v of this (clip, head): lanes 0-7 / 8-15 / 16-23 load 8 values each (sc1: handed off)
             if (lane < 24) {
                 const int part = lane >> 3, e0 = (lane & 7) * 8;
@@ -645,15 +846,18 @@ struct BdecCtx {
             float qv[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) qv[e] = qs[lane8 * 8 + e];
-            constexpr int U = 8;
-            const u32x4 zero = {0, 0, 0, 0};
             float lmax = -INFINITY;
             for (int t0 = grp; t0 < pos; t0 += 8 * U) {
                 u32x4 raw[U];
+                if (t0 == grp) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int tt = t0 + 8 * u;
-                    raw[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(K + (long)tt * 64 + lane8 * 8)) : zero;
+                    for (int u = 0; u < U; u++) raw[u] = rk[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const int tt = t0 + 8 * u;
+                        raw[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(K + (long)tt * 64 + lane8 * 8)) : zero;
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
@@ -697,10 +901,15 @@ struct BdecCtx {
             for (int e = 0; e < 8; e++) acc[e] = 0.0f;
             for (int t0 = grp; t0 < pos; t0 += 8 * U) {
                 u32x4 raw[U];
+                if (t0 == grp) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int tt = t0 + 8 * u;
-                    raw[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(V + (long)tt * 64 + lane8 * 8)) : zero;
+                    for (int u = 0; u < U; u++) raw[u] = rv[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const int tt = t0 + 8 * u;
+                        raw[u] = tt < pos ? __builtin_nontemporal_load((const u32x4*)(V + (long)tt * 64 + lane8 * 8)) : zero;
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
@@ -736,13 +945,26 @@ struct BdecCtx {
         return true;
     }
 
-    // ---- H5: Q'_h = s Wk_h^T q_h (hi + lo) for (row group, head h, half b of the d columns) -----------------
+    // ---- H6: Q'_h = s Wk_h^T q_h (hi + lo) for (row group, head h, half b of the d columns) -----------------
+    // The task's Wk_h^T fragments (NPW column tiles per wave) are loaded before the hand-off wait.
     __device__ bool qproj(int layer, CLayer& Lw) {
+        BD_LOCALS;
         const int j = cw, h = j >> 1, half = j & 1;
-        if (!wait(layer, PH_H4)) return false;
-        stamp(PH_H5, 0);
-        if (j >= 2 * H) return true;
+        const bool task = j < 2 * H;
+        constexpr int NCT = D / 2 / 16, NPW = NCT / 4;  // column tiles of the half, per wave
         const T* wkt = (const T*)Lw.wkt;  // [H][D][64]
+        FT wf[NPW][2];
+        if (task) {
+#pragma unroll
+            for (int u = 0; u < NPW; u++)
+#pragma unroll
+                for (int ks = 0; ks < 2; ks++)
+                    wf[u][ks] = *(const FT*)(wkt + ((long)h * D + half * (D / 2) + (wave + 4 * u) * 16 + (lane & 15)) * 64 + ks * 32 +
+                                             8 * (lane >> 4));
+        }
+        if (!wait(layer, PH_H5)) return false;
+        stamp(PH_H6, 0);
+        if (!task) return true;
         const rsrc_t rq = mkr(a.bxq, (long)a.M * D * 2);
         FT qf[2][2];
 #pragma unroll
@@ -752,18 +974,15 @@ struct BdecCtx {
                 const int m = r0 + rt * 16 + (lane & 15);
                 qf[rt][ks] = __builtin_bit_cast(FT, ld16(rq, (uint32_t)(((long)m * D + h * 64 + ks * 32 + 8 * (lane >> 4)) * 2)));
             }
-        constexpr int NCT = D / 2 / 16;  // column tiles of the half
         T* qx = (T*)a.qx;
-        for (int ct = wave; ct < NCT; ct += 4) {
-            const int c0 = half * (D / 2) + ct * 16;
-            FT wf[2];
 #pragma unroll
-            for (int ks = 0; ks < 2; ks++) wf[ks] = *(const FT*)(wkt + ((long)h * D + c0 + (lane & 15)) * 64 + ks * 32 + 8 * (lane >> 4));
+        for (int u = 0; u < NPW; u++) {
+            const int c0 = half * (D / 2) + (wave + 4 * u) * 16;
 #pragma unroll
             for (int rt = 0; rt < 2; rt++) {
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(wf[ks], qf[rt][ks], acc);
+                for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(wf[u][ks], qf[rt][ks], acc);
                 const int m = r0 + rt * 16 + (lane & 15);
                 if (m >= a.M) continue;
                 const int c = c0 + 4 * (lane >> 4);
@@ -779,7 +998,7 @@ struct BdecCtx {
                 *(u32x2*)(qx + ((long)m * 2 * H + H + h) * D + c) = pack4<T>(lo);
             }
         }
-        stamp(PH_H5, 1);
+        stamp(PH_H6, 1);
         return true;
     }
 };
@@ -798,26 +1017,23 @@ __global__ void __launch_bounds__(kNT, 1) bdec_kernel(const BdecArgs a) {
         CLayer& W = LT[A.la];
         const int l = A.la;
         if (!C.combine(l, W)) return;
-        if (!C.template gemm<BE_RESID, AS_T>(l, PH_T2, l, PH_T1, (const T*)W.wxo, W.bxo, d, d, (const T*)A.batt, nullptr, nullptr, A.x, d)) return;
-        if (!C.template gemm<BE_GELU, AS_LN>(l, PH_T3, l, PH_T2, (const T*)W.w1, W.b1, 4 * d, d, (const T*)A.x, W.ln2_w, W.ln2_b, A.bff, 4 * d)) return;
-        if (!C.template gemm<BE_RESID, AS_T>(l, PH_T4, l, PH_T3, (const T*)W.w2, W.b2, d, 4 * d, (const T*)A.bff, nullptr, nullptr, A.x, d)) return;
+        if (!C.template gemm<BE_RESID, AS_T>(l, PH_T2, l, PH_T1, (const T*)W.wxo, W.bxo, d, d, A.batt, A.x, d)) return;
+        if (!C.template gemm<BE_GELU, AS_LN>(l, PH_T4, l, PH_T2, (const T*)W.w1, W.b1, 4 * d, d, A.x, A.bff, 4 * d, W.ln2_w, W.ln2_b)) return;
+        if (!C.template gemm<BE_RESID, AS_T>(l, PH_T5, l, PH_T4, (const T*)W.w2, W.b2, d, 4 * d, A.bff, A.x, d)) return;
     }
     if (A.lb < A.L) {
         CLayer& W = LT[A.lb];
         const int l = A.lb;
         bool ok;
-        if (A.la < 0) ok = C.template gemm<BE_QKV, AS_EMB>(l, PH_H1, 0, -1, (const T*)W.wqkv, W.bqkv, 3 * d, d, nullptr, W.ln1_w, W.ln1_b, A.bq, 3 * d);
-        else ok = C.template gemm<BE_QKV, AS_LN>(l, PH_H1, A.la, PH_T4, (const T*)W.wqkv, W.bqkv, 3 * d, d, (const T*)A.x, W.ln1_w, W.ln1_b, A.bq, 3 * d);
+        if (A.la < 0) ok = C.template gemm<BE_QKV, AS_EMB>(l, PH_H1, 0, -1, (const T*)W.wqkv, W.bqkv, 3 * d, d, A.x, A.bq, 3 * d, W.ln1_w, W.ln1_b);
+        else ok = C.template gemm<BE_QKV, AS_LN>(l, PH_H1, A.la, PH_T5, (const T*)W.wqkv, W.bqkv, 3 * d, d, A.x, A.bq, 3 * d, W.ln1_w, W.ln1_b);
         if (!ok) return;
         if (!C.self_attn(l)) return;
-        if (!C.template gemm<BE_RESID, AS_T>(l, PH_H3, l, PH_H2, (const T*)W.wo, W.bo, d, d, (const T*)A.batt, nullptr, nullptr, A.x, d)) return;
-        if (!C.template gemm<BE_SCALE, AS_LN>(l, PH_H4, l, PH_H3, (const T*)W.wxq, W.bxq, d, d, (const T*)A.x, W.lnx_w, W.lnx_b, A.bxq, d)) return;
+        if (!C.template gemm<BE_RESID, AS_T>(l, PH_H3, l, PH_H2, (const T*)W.wo, W.bo, d, d, A.batt, A.x, d)) return;
+        if (!C.template gemm<BE_SCALE, AS_LN>(l, PH_H5, l, PH_H3, (const T*)W.wxq, W.bxq, d, d, A.x, A.bxq, d, W.lnx_w, W.lnx_b)) return;
         C.qproj(l, W);
-    } else if (C.cw == 0) {  // the final LayerNorm of the row group (the logits GEMM's input)
-        if (!C.wait(A.la, PH_T4)) return;
-        C.stamp(PH_H5, 0);
-        C.load_a_ln(A.x, false, A.lnd_w, A.lnd_b, false, (T*)A.out_dh);
-        C.stamp(PH_H5, 1);
+    } else {  // the final LayerNorm (the logits GEMM's input; counters of the spare layer slot L)
+        C.ln_phase(A.L, PH_H0, A.la, PH_T5, false, A.lnd_w, A.lnd_b, (T*)A.out_dh);
     }
 }
 
