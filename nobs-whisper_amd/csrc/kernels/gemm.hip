@@ -1648,6 +1648,19 @@ static void launch_splitk_reduce(const GemmArgs& g, int splits, hipStream_t st) 
     splitk_reduce_kernel<T, EPI><<<std::min<long>(4096, cdiv(work, thr)), thr, 0, st>>>(g, splits);
 }
 
+// The encoder GEMMs' tile order (gemm8p_kernel gm). Row-major (n fastest) lets the 32 workgroups an XCD
+// runs at once cover ~1.6 m-tiles x 20 n-tiles of FC1, so every B tile is fetched by every XCD for every
+// m-tile; groups of 4 m-tiles make them a 4 x 8 block. Measured (large-v3, 128 x 30 s, rocprofv3
+// FETCH_SIZE x2, profiles/r05_gemm_gm_pmc.txt): FC1 2068 -> 1111 MB per launch, QKV 1243 -> 848 MB; the
+// d-wide GEMMs (5 n-tiles) fetched more (857 -> 987 MB), and stay row-major. The encode phase time does not
+// move (321.3 / 320.1 / 324.0 / 331.8 ms at gm 0 / 4 / 8 / 16): the kernel is bound by its MFMA / LDS
+// schedule, not by L2 misses.
+static int gemm_group_m(int tiles_n) {
+    static const int env = getenv("WHISPER_MI355X_GEMM_GM") ? atoi(getenv("WHISPER_MI355X_GEMM_GM")) : -1;
+    if (env >= 0) return env;
+    return tiles_n >= 8 ? 4 : 0;
+}
+
 template <typename T, int EPI>
 static void launch_t(const GemmArgs& g, hipStream_t st) {
     if (g.w8_scale) {  // e4m3 weights: the decode-step split-K kernel only
@@ -1660,7 +1673,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int tn = cdiv(g.N, 256);
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
-        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, 0);
+        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, gemm_group_m(tn));
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
