@@ -1,5 +1,6 @@
 """GPU: time of the direct cross-attention kernels (Q' projection + step + combine, debug hook) on the
-large-v3 decode shape: n tokens (one clip each) x 1500 encoder rows x d, and the HBM rate on E."""
+large-v3 decode shape: n tokens (one clip each) x 1500 encoder rows x d, and the HBM rate on E.
+SAMESLOT=1: every clip reads the same E (cache-resident): the kernel's rate without the HBM stream."""
 import ctypes as C
 import os
 import sys
@@ -17,7 +18,7 @@ d, Tn = int(os.environ.get("D", "1280")), 1500
 H = d // 64
 rng = np.random.default_rng(0)
 for n in [int(x) for x in os.environ.get("NS", "128,64").split(",")]:
-    arrs = [(rng.standard_normal((n, Tn, d)) * 0.5).astype(np.float16).view(np.uint16), np.arange(n, dtype=np.int32),
+    arrs = [(rng.standard_normal((n, Tn, d)) * 0.5).astype(np.float16).view(np.uint16), (np.zeros(n, np.int32) if os.environ.get("SAMESLOT") else np.arange(n, dtype=np.int32)),
             rng.standard_normal((n, d)).astype(np.float16).view(np.uint16),
             (rng.standard_normal((H, d, 64)) / 30).astype(np.float16).view(np.uint16),
             (rng.standard_normal((d, d)) / 30).astype(np.float16).view(np.uint16), np.zeros(d, np.float32)]
