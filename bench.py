@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0       # dense bf16/f16 MFMA peak (no sparsity)
 FP8_PEAK_TFS = 5000.0        # dense fp8 MFMA peak
 # PMC traffic pass of the roofline kernel (tools/pmc.sh -> tools/pmc_traffic.py), chosen by name
-PMC_TRAFFIC_FILE = "r04_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r05_pmc_traffic.json"
 KT_LAYER_STRIDE = 8
 
 
@@ -394,7 +394,7 @@ def main():
     ap.add_argument("--inflight-line", type=int, default=1,
                     help="with --variants: also a serving line with two batches in flight (two states)")
     ap.add_argument("--f16-line", type=int, default=1,
-                    help="with --dtype bf16: also time the same config with f16 weights (the token-exact path)")
+                    help="with --dtype bf16: also time the same config with f16 weights (the path exact against the oracle up to its near ties)")
     ap.add_argument("--fallback-line", type=int, default=0,
                     help="also time the reference's verbatim FullParams with temperature fallback (slow on "
                          "untrained weights: most windows fall back to sampled re-decodes)")
@@ -623,7 +623,7 @@ def main():
                                  ms_per_step=round(1e3 * el / args.variant_steps, 2), pcie_inclusive=True))
             del host_pcm
 
-    # the f16 engine on the same config: whisper.cpp's own weight type, the token-exact parity path
+    # the f16 engine on the same config: whisper.cpp's own weight type, the parity path (exact against the oracle up to its near ties)
     # (tests/test_gpu_fulldepth.py); bf16 is the headline dtype BASELINE names. One GPU only.
     if args.f16_line and args.dtype == "bf16" and nb and world == 1:
         ctx16 = wrs.WhisperContext(model_path, dtype=wrs.F16, gpu_device=local_rank)
@@ -641,7 +641,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el = max_over_ranks(time.time() - t0, dist, "cuda")
-        variants.append(dict(workload="f16 weights (the GGML file's own type; token-exact against the oracle), "
+        variants.append(dict(workload="f16 weights (the GGML file's own type; exact against the oracle up to its near ties), "
                                       "same chunks and fixed-work decode, language en, no prompt", dtype="f16",
                              value=round(30.0 * global_batch * args.variant_steps / el, 2),
                              ms_per_step=round(1e3 * el / args.variant_steps, 2),
