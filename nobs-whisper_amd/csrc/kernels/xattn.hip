@@ -151,7 +151,11 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
     constexpr int TILE = 16 * RC;        // u32x4 per 16-row tile
     constexpr int NH = (H + 15) / 16;    // score column tiles holding the hi columns (0..H-1)
     constexpr int RSR = 16 * NH + 4;     // f32 row stride of the score partials (bank spread)
-    constexpr int STG_B = NS * TILE * 16, RED_B = NW * 16 * RSR * 4, P_B = 32 * 16 * (int)sizeof(T);
+    // P image [32 heads][PS] T, rows 0..15 of a head contiguous; PS = 20 (not 16): the P.V operand reads of 32
+    // lanes (one head each, 8 bytes at rows 4 hh and 8 + 4 hh) then hit 32 distinct bank pairs (head stride 10
+    // dwords) instead of 4-way conflicting at a stride of 8 dwords
+    constexpr int PS = 20;
+    constexpr int STG_B = NS * TILE * 16, RED_B = NW * 16 * RSR * 4, P_B = 32 * PS * (int)sizeof(T);
     static_assert(RC % 16 == 0, "d must be a multiple of 128");
     static_assert(H * 16 <= NW * 64, "one softmax lane per (head, row)");
     static_assert(H <= 32, "heads are the N = 32 side of the P.V MFMA");
@@ -159,7 +163,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
     __shared__ __attribute__((aligned(16))) char lds[STG_B + RED_B + P_B + 32 * 4 + 16];
     u32x4* stg = (u32x4*)lds;
     float* red = (float*)(lds + STG_B);
-    T* pimg = (T*)(lds + STG_B + RED_B);              // P [head][16 rows]
+    T* pimg = (T*)(lds + STG_B + RED_B);              // P [head][PS] (rows 0..15 used)
     float* alph = (float*)(lds + STG_B + RED_B + P_B);  // per-head rescale of the tile
     int* flag = (int*)(alph + 32);                      // [2]: some head rescaled at tile t (parity t&1)
 
@@ -170,7 +174,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
     const T* E = enc + (long)slot[i] * Tn * D;
     const int cw = wave * CT * 32;  // this wave's first column
 
-    for (int e = tid; e < 32 * 16; e += NW * 64) pimg[e] = (T)0.0f;
+    for (int e = tid; e < 32 * PS; e += NW * 64) pimg[e] = (T)0.0f;
     if (tid < 32) alph[tid] = 1.0f;
     if (tid < 2) flag[tid] = 0;
 
@@ -289,7 +293,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
             }
             const T pt = (T)__builtin_amdgcn_exp2f(s2 - m_run);
             l_run = l_run * alpha + sum16((float)pt);
-            pimg[h * 16 + r] = pt;
+            pimg[h * PS + r] = pt;
             if (r == 0) alph[h] = alpha;
         }
         if (tid == 0) flag[(t + 1) & 1] = 0;  // last read in tile t-1's P.V, before B1
@@ -303,7 +307,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
         // before the one wait.
         FT pf;
         {
-            const T* pr = pimg + (lane & 31) * 16 + 4 * hh;
+            const T* pr = pimg + (lane & 31) * PS + 4 * hh;
             const v4s lo = *(const v4s*)pr;
             const v4s hi = *(const v4s*)(pr + 8);
             pf = __builtin_bit_cast(FT, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
