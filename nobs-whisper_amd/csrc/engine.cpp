@@ -297,6 +297,9 @@ static void free_ws(Workspace& w) {
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
     dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync); dfree(w.bd_sync); dfree(w.bq); dfree(w.bhn);
     if (w.h_pd_err) hipHostFree(w.h_pd_err);
+    if (w.h_ring) hipHostFree(w.h_ring);
+    for (auto& e : w.ring_ev)
+        if (e) hipEventDestroy(e);
     if (w.h_ints) hipHostFree(w.h_ints);
     if (w.h_qtiles) hipHostFree(w.h_qtiles);
     if (w.h_tout) hipHostFree(w.h_tout);
@@ -383,6 +386,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
         dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.mel_ptrs);
         dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles); dfree(w.bq); dfree(w.bhn);
+        if (w.h_ring) { WM_CHECK(hipHostFree(w.h_ring)); w.h_ring = nullptr; w.ring = nullptr; }
         for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
             if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
         w.cap_jobs = w.cap_tok = w.cap_cross = w.cap_xq = 0;
@@ -1735,21 +1739,22 @@ static void run_logits(Sched& S, const std::vector<int>& act, bool want_nosp, st
 // holding CUs would otherwise cost the 50 ms timeout on every step)
 static const double kPdecBackoffMs = 1000.0;
 
-static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::vector<float>>& probs_rows) {
-    Context* c = S.c;
-    whisper_state* s = S.s;
-    const int n = (int)act.size();
-    decoder_upload(c, s, n, n, false);
-    const bool any = logits_prepare(S, act, false);
-    whisper_state::DecGraph* G = nullptr;
+// the persistent launch's error word on the device (null for the launch chain)
+static const unsigned* pd_err_ptr(Context* c, whisper_state* s, int pd) {
+    const Hparams& hp = c->hp;
+    Workspace& w = s->ws;
+    if (pd == 1) return (const unsigned*)((const char*)w.pd_sync + pdec_granules(hp.n_text_state, hp.n_text_layer, hp.n_text_head).err_bytes);
+    if (pd == 2) return w.bd_sync + bdec_err_index(hp.n_text_layer);
+    return nullptr;
+}
+static size_t ring_slot_bytes(const Workspace& w) { return (size_t)w.cap_jobs * sizeof(TokOut) + 16; }
+
+// The decode graph of n rows on the state's current path (pd: 0 launch chain, 1 persistent step, 2 batched
+// chain), instance `par` (captured on first use; graphs of a persistent path captured under an older stamps
+// pointer / spin limit are retired first). par 0: the per-step path's; par 1, 2: the pipelined path's two
+// instances, which end with the device-side advance writing the step's results to ring slot par - 1.
+static whisper_state::DecGraph* dec_graph(Context* c, whisper_state* s, int n, int pd, int par) {
     const int sig = dec_path_sig();
-    const double t_step = now_ms();
-    s->pdec_off = s->pdec_give_ups > 0 && t_step < s->pdec_off_until;
-    s->step_rows = n;
-    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
-    if (pd == 1) pdec_prepare(c, s);
-    if (pd == 2) bdec_prepare(c, s);
-    // retire persistent-step graphs captured under an older stamps pointer / spin limit (g_pdec_gen)
     for (size_t i = 0; i < s->dec_graphs.size();) {
         auto& g = s->dec_graphs[i];
         if (g.pdec && g.gen != g_pdec_gen) {
@@ -1761,22 +1766,52 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
         }
     }
     for (auto& g : s->dec_graphs)
-        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd)
-            G = &g;
-    if (!G) {
-        whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, g_pdec_gen, nullptr, {}};
-        hipGraph_t graph;
-        s->capture_ev = &g.ev;
-        WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        decoder_launch(c, s, n, n, true, s->direct);
-        logits_launch(c, s, n);
-        WM_CHECK(hipStreamEndCapture(s->stream, &graph));
-        s->capture_ev = nullptr;
-        WM_CHECK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
-        WM_CHECK(hipGraphDestroy(graph));
-        s->dec_graphs.push_back(std::move(g));
-        G = &s->dec_graphs.back();
+        if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd &&
+            g.par == par)
+            return &g;
+    whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, g_pdec_gen, par, nullptr, {}};
+    hipGraph_t graph;
+    s->capture_ev = &g.ev;
+    WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+    decoder_launch(c, s, n, n, true, s->direct);
+    logits_launch(c, s, n);
+    if (par > 0) {
+        Workspace& w = s->ws;
+        char* slot = w.ring + (par - 1) * ring_slot_bytes(w);
+        launch_decode_advance(n, w.cap_tok, c->vid.beg, w.tout, w.tok, w.ctl, (TokOut*)slot, pd_err_ptr(c, s, pd),
+                              (unsigned*)(slot + (size_t)w.cap_jobs * sizeof(TokOut)), s->stream);
     }
+    WM_CHECK(hipStreamEndCapture(s->stream, &graph));
+    s->capture_ev = nullptr;
+    WM_CHECK(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+    WM_CHECK(hipGraphDestroy(graph));
+    s->dec_graphs.push_back(std::move(g));
+    return &s->dec_graphs.back();
+}
+
+// persistent launches (the one-launch step, the chain) of different states of this process on one device never
+// overlap: two of them could hold half the CUs each
+static std::mutex g_pdec_run_mu[16];
+
+// the decode path of a step of n rows (and its buffers prepared)
+static int dec_path_prepare(Context* c, whisper_state* s, int n) {
+    s->pdec_off = s->pdec_give_ups > 0 && now_ms() < s->pdec_off_until;
+    s->step_rows = n;
+    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
+    if (pd == 1) pdec_prepare(c, s);
+    if (pd == 2) bdec_prepare(c, s);
+    return pd;
+}
+
+static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::vector<float>>& probs_rows) {
+    Context* c = S.c;
+    whisper_state* s = S.s;
+    const int n = (int)act.size();
+    decoder_upload(c, s, n, n, false);
+    const bool any = logits_prepare(S, act, false);
+    const double t_step = now_ms();
+    const int pd = dec_path_prepare(c, s, n);
+    whisper_state::DecGraph* G = dec_graph(c, s, n, pd, 0);
     if (!G->pdec) {
         WM_CHECK(hipGraphLaunch(G->exec, s->stream));
         logits_finish(S, n, any, probs_rows);
@@ -1786,10 +1821,9 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     // A persistent launch (the one-launch step, or the chain's launches) needs its 256 workgroups resident
     // together: persistent steps of different states (threads) of this process on one device never overlap,
     // so two of them cannot hold half the CUs each (steps on different devices do not wait for each other)
-    static std::mutex pdec_run_mu[16];
     bool gave_up;
     {
-        std::lock_guard<std::mutex> lk(pdec_run_mu[c->device & 15]);
+        std::lock_guard<std::mutex> lk(g_pdec_run_mu[c->device & 15]);
         WM_CHECK(hipGraphLaunch(G->exec, s->stream));
         logits_finish(S, n, any, probs_rows);
         gave_up = *s->ws.h_pd_err != 0;
@@ -1818,6 +1852,193 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     g_pdec_give_ups_total++;
     s->pdec_off_until = now_ms() + kPdecBackoffMs;
     s->pdec_lost_ms += now_ms() - t_step;
+}
+
+// Pipelined greedy decoding. The per-step path waits for a step's 32-byte results before it launches the next
+// step, so every step pays the host's round trip (copy, synchronise, process_step, upload, launch: ~40-60 us,
+// a fifth of a base-model persistent step). Here a small kernel advances every row's input token, position and
+// logits-rule state on the device after the step (launch_decode_advance: the token the logits kernel chose, as
+// process_step + fill_ctl would), the next step's graph is launched at once, and the host processes step k
+// while step k + 1 runs. The results are the per-step path's bits: the same graphs on the same inputs. A row
+// whose attempt ends at step k has had step k + 1 computed for it (its self-K/V row at the next position, never
+// read: a new attempt prefills over it); the other rows' step k + 1 results are used, since a row's results
+// do not depend on the other rows. Taken only where the host has nothing to decide per step: greedy attempts
+// (no sampling), no forced tokens or logits hooks, no other job in another phase, and attempts that already
+// decoded pipe_min_step() tokens (24; the speculative step at an attempt's end costs one step, which pays off only
+// over a long attempt). WHISPER_MI355X_PIPE=0 turns it off.
+static int pipe_min_step() {  // kPipeMinStep, or WHISPER_MI355X_PIPE_MIN (tests: exercise short attempts)
+    const char* e = getenv("WHISPER_MI355X_PIPE_MIN");
+    return e ? atoi(e) : 24;
+}
+static bool pipe_on() {  // (read per call: tests compare both paths in one process)
+    const char* e = getenv("WHISPER_MI355X_PIPE");
+    return !e || atoi(e) != 0;
+}
+
+static bool pipe_ok(Sched& S, const std::vector<int>& act) {
+    if (!pipe_on() || S.o.forced || (S.o.spot_logits && S.o.n_spot > 0)) return false;
+    for (size_t k = 0; k < S.jobs.size(); k++) {
+        const Job& j = S.jobs[k];
+        if (j.phase == PH_DONE) continue;
+        if (j.phase != PH_DECODE) return false;
+        if (S.temps[j.temp_idx] >= 1e-6f || j.step < pipe_min_step()) return false;
+    }
+    return !act.empty();
+}
+
+// Everything about a decode step of n rows that can change a row's bits with n: the path (persistent step,
+// batched chain, small-M GEMMs, launch chain), the cache-form cross-attention kernel (the wide one up to
+// attn_cross_wide_max() rows) and the direct form's key-split count (xattn_splits). Equal keys: a row's
+// results at n and at n' rows are the same bits.
+static long step_variant(Context* c, whisper_state* s, int n) {
+    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
+    const bool small = (c->quant && n <= quant_small_max()) || n <= small_m_max();
+    const bool wide = !s->direct && n <= attn_cross_wide_max();
+    const int sp = s->direct ? xattn_splits(n, c->hp.n_audio_ctx) : 0;
+    return pd | (long)small << 2 | (long)wide << 3 | (long)sp << 4;
+}
+
+// the host inputs of a decode step of the `act` jobs (their next token, position, slot, logits row)
+static void step_inputs(Sched& S, const std::vector<int>& act) {
+    Workspace& w = S.s->ws;
+    int* hi = w.h_ints;
+    for (int r = 0; r < (int)act.size(); r++) {
+        const Job& j = S.jobs[act[r]];
+        hi[r] = j.tokens.back().id;
+        hi[w.cap_tok + r] = (int)j.prompt.size() + j.step;
+        hi[2 * w.cap_tok + r] = j.slot;
+        hi[5 * w.cap_tok + r] = r;
+    }
+}
+
+// Re-run the step of the `act` rows on the per-kernel path after its persistent launch gave up (the device
+// inputs as uploaded by `upload`); results in w.h_tout. Counted like decode_step's give-ups.
+static void pipe_give_up(Sched& S, const std::vector<int>& act, bool upload, double t0) {
+    Context* c = S.c;
+    whisper_state* s = S.s;
+    const int n = (int)act.size();
+    WM_CHECK(hipStreamSynchronize(s->stream));
+    static bool warned = false;
+    if (!warned) fprintf(stderr, "whisper_mi355x: persistent decode step timed out; step re-run on the per-kernel path\n");
+    warned = true;
+    if (upload) {
+        step_inputs(S, act);
+        decoder_upload(c, s, n, n, false);
+        logits_prepare(S, act, false);
+    }
+    *s->ws.h_pd_err = 0;
+    std::vector<std::vector<float>> probs_rows;
+    s->pdec_block = true;
+    try {
+        decoder_launch(c, s, n, n, true, s->direct);
+        logits_launch(c, s, n);
+        logits_finish(S, n, false, probs_rows);
+    } catch (...) {
+        s->pdec_block = false;
+        throw;
+    }
+    s->pdec_block = false;
+    s->pdec_give_ups++;
+    g_pdec_give_ups_total++;
+    s->pdec_off_until = now_ms() + kPdecBackoffMs;
+    s->pdec_lost_ms += now_ms() - t0;
+}
+
+// Decode the `act` jobs step after step with the next step in flight while the host processes the last one,
+// until an attempt ends (or the caller's abort callback fires); every step it ran is processed before it
+// returns, so the jobs are left exactly as the per-step path leaves them.
+static void decode_pipelined(Sched& S, const std::vector<int>& act) {
+    Context* c = S.c;
+    whisper_state* s = S.s;
+    Workspace& w = s->ws;
+    const whisper_full_params& p = S.p;
+    const int n = (int)act.size();
+    hipStream_t st = s->stream;
+    const size_t slot_b = ring_slot_bytes(w);
+    if (!w.h_ring) {  // written by the advance kernel over the bus (coherent pinned memory), read after the event
+        WM_CHECK(hipHostMalloc((void**)&w.h_ring, 2 * slot_b, hipHostMallocCoherent | hipHostMallocMapped));
+        WM_CHECK(hipHostGetDevicePointer((void**)&w.ring, w.h_ring, 0));
+    }
+    for (auto& e : w.ring_ev)
+        if (!e) WM_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    step_inputs(S, act);
+    decoder_upload(c, s, n, n, false);
+    logits_prepare(S, act, false);
+    const int pd = dec_path_prepare(c, s, n);
+    dec_graph(c, s, n, pd, 1);
+    dec_graph(c, s, n, pd, 2);  // (may grow dec_graphs: the pointers are taken after both exist)
+    whisper_state::DecGraph* G[2] = {dec_graph(c, s, n, pd, 1), dec_graph(c, s, n, pd, 2)};
+    std::unique_lock<std::mutex> lk(g_pdec_run_mu[c->device & 15], std::defer_lock);
+    if (pd) lk.lock();
+    double t_step = now_ms();
+    WM_CHECK(hipGraphLaunch(G[0]->exec, st));
+    WM_CHECK(hipEventRecord(w.ring_ev[0], st));
+    for (int k = 0;; k++) {
+        const int par = k & 1;
+        char* hslot = w.h_ring + par * slot_b;
+        // step k produces token j.step + 1 of each job; a job continues past it only if j.step + 2 < n_max
+        bool more = false;
+        for (int r = 0; r < n; r++) more |= S.jobs[act[r]].step + 2 < S.n_max_steps;
+        if (more) {
+            WM_CHECK(hipGraphLaunch(G[par ^ 1]->exec, st));
+            WM_CHECK(hipEventRecord(w.ring_ev[par ^ 1], st));
+        }
+        s->cur_self_work += (double)n * c->hp.n_text_head * 64 * 2 * 2;  // (kernel timing: one more key per row)
+        WM_CHECK(hipEventSynchronize(w.ring_ev[par]));
+        kt_flush_graph(s, *G[par]);
+        const TokOut* out = (const TokOut*)hslot;
+        if (pd && *(const unsigned*)(hslot + (size_t)w.cap_jobs * sizeof(TokOut))) {
+            // step k gave up: re-run it on the per-kernel path from the host's inputs, then leave
+            pipe_give_up(S, act, true, t_step);
+            for (int r = 0; r < n; r++) S.jobs[act[r]].step++;
+            for (int r = 0; r < n; r++) {
+                Job& j = S.jobs[act[r]];
+                if (!process_step(S, j, w.h_tout[r], nullptr)) attempt_done(S, j);
+            }
+            return;
+        }
+        for (int r = 0; r < n; r++) S.jobs[act[r]].step++;
+        bool ended = false;
+        for (int r = 0; r < n; r++) {
+            Job& j = S.jobs[act[r]];
+            if (!process_step(S, j, out[r], nullptr)) {
+                attempt_done(S, j);
+                ended = true;
+            }
+        }
+        const bool aborted = p.abort_callback && p.abort_callback(p.abort_callback_user_data);
+        if (!ended && !aborted && more) {
+            t_step = now_ms();
+            continue;
+        }
+        if (more) {
+            // step k + 1 ran for every row: its results stand for the rows still decoding if a step of that
+            // many rows computes the same bits (step_variant); otherwise the main loop runs step k + 1 again
+            // for them from the host's inputs (the speculative one only wrote their self-K/V rows at the
+            // next position, which the re-run writes again)
+            WM_CHECK(hipMemcpyAsync(w.h_tout, w.tout, (size_t)n * sizeof(TokOut), hipMemcpyDeviceToHost, st));
+            WM_CHECK(hipStreamSynchronize(st));
+            kt_flush_graph(s, *G[par ^ 1]);
+            std::vector<int> still;
+            for (int r = 0; r < n; r++)
+                if (S.jobs[act[r]].phase == PH_DECODE) still.push_back(r);
+            if (still.empty() || step_variant(c, s, (int)still.size()) != step_variant(c, s, n)) {
+                if (pd) *w.h_pd_err = 0;  // (a discarded step's give-up is not one)
+                return;
+            }
+            if (pd && *w.h_pd_err) {
+                // its persistent launch gave up: the step again, for all n rows, from the host's inputs (the
+                // graph's own advance has moved the device's past step k + 1)
+                pipe_give_up(S, act, true, now_ms());
+            }
+            for (int r : still) {
+                Job& j = S.jobs[act[r]];
+                j.step++;
+                if (!process_step(S, j, w.h_tout[r], nullptr)) attempt_done(S, j);
+            }
+        }
+        return;
+    }
 }
 
 // Batches above kPairMin clips run as two independent halves at
@@ -2106,7 +2327,12 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
         {
             std::vector<int> act;
             for (int k = 0; k < n_jobs; k++) if (S.jobs[k].phase == PH_DECODE) act.push_back(k);
-            if (!act.empty()) {
+            if (!act.empty() && pipe_ok(S, act)) {
+                if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
+                const double td = now_ms();
+                decode_pipelined(S, act);
+                S.t_decode += now_ms() - td;
+            } else if (!act.empty()) {
                 if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
                 const double td = now_ms();
                 int* hi = w.h_ints;

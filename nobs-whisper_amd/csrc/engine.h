@@ -174,6 +174,11 @@ struct Workspace {
     // (shared with the batched chain's error word)
     unsigned* pd_sync = nullptr;
     unsigned* h_pd_err = nullptr;
+    // pipelined greedy decoding (engine.cpp decode_pipelined): two ring slots of [cap_jobs TokOut][16-byte error
+    // word] on the device and in pinned host memory, and the event after each slot's copy
+    char* ring = nullptr;
+    char* h_ring = nullptr;
+    hipEvent_t ring_ev[2] = {nullptr, nullptr};
     // batched persistent chain (kernels/bdec.hip): its counters + error word, and the q|k|v rows [cap][3d]
     unsigned* bd_sync = nullptr;
     void* bq = nullptr;
@@ -240,7 +245,9 @@ struct whisper_state {
     // (gen: g_pdec_gen when a persistent step was captured; its graph holds the stamps pointer and spin limit of
     // that time, so a setter call retires it)
     // pdec: 0 = launch chain, 1 = the persistent step (kernels/pdec.hip), 2 = the batched chain (kernels/bdec.hip)
-    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; int pdec; int gen; hipGraphExec_t exec; std::vector<KPending> ev; };
+    // (par: 0 for the per-step path; the pipelined path alternates two instances, 0 and 1, so that one step's
+    // graph events are read while the other instance runs)
+    struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; int pdec; int gen; int par; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
     double cur_self_work = 0;                     // self-attention bytes of the current step

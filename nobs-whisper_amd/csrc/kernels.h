@@ -323,5 +323,9 @@ struct TokOut { int id, tid; float p, plog, pt, ptsum, nosp_prob, pad; };
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v,
                    TokOut* out, float* probs, void* rec, hipStream_t st);
 size_t logits_rec_bytes(int n_seq);
+// pipelined greedy decoding: advance every row's input token, position and SeqCtl on the device after a step
+// and copy its TokOut (+ the persistent launch's error word, if err) to a ring slot (kernels/logits.hip)
+void launch_decode_advance(int n, int ct, int beg, const TokOut* tout, int* ints, SeqCtl* ctl, TokOut* ring,
+                           const unsigned* err, unsigned* ring_err, hipStream_t st);
 
 }  // namespace wm

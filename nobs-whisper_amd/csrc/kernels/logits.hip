@@ -429,4 +429,42 @@ void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, c
     logits_kernel<<<n_seq, LT, (size_t)NPT_LDS * LT * sizeof(float), st>>>(logits, ld, ctl, v, out, probs);
 }
 
+// ---- device-side step advance (pipelined greedy decoding, engine.cpp decode_pipelined) -----------------------
+// After a decode step's logits kernel, in stream order: row r's chosen token becomes its next input and its
+// position advances (the layout of decoder_upload: tok | pos | slot | nkv_self | nkv_cross, ct entries each),
+// its SeqCtl advances exactly as fill_ctl would rebuild it from the job after process_step appended the
+// token (is_initial, last_ts = id >= beg, penult_ts = the previous last_ts or true after the first token;
+// has_ts / seek_delta from a timestamp above beg), and the step's TokOut (and the persistent launch's error
+// word) is copied to the ring slot the host reads while the next step runs.
+__global__ void decode_advance_kernel(int n, int ct, int beg, const TokOut* __restrict__ tout, int* __restrict__ ints,
+                                      SeqCtl* __restrict__ ctl, TokOut* __restrict__ ring, const unsigned* __restrict__ err,
+                                      unsigned* __restrict__ ring_err) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0) *ring_err = err ? *err : 0u;
+    if (r >= n) return;
+    const TokOut o = tout[r];
+    ring[r] = o;
+    const int id = o.id;
+    ints[r] = id;                       // tok
+    const int pos = ints[ct + r] + 1;   // pos
+    ints[ct + r] = pos;
+    ints[3 * ct + r] = pos + 1;         // nkv_self
+    SeqCtl c = ctl[r];
+    c.penult_ts = c.is_initial ? 1 : c.last_ts;
+    c.last_ts = id >= beg;
+    c.is_initial = 0;
+    if (id > beg) {
+        c.has_ts = 1;
+        c.seek_delta = 2 * (id - beg);
+    }
+    c.want_nosp = 0;
+    ctl[r] = c;
+}
+
+void launch_decode_advance(int n, int ct, int beg, const TokOut* tout, int* ints, SeqCtl* ctl, TokOut* ring,
+                           const unsigned* err, unsigned* ring_err, hipStream_t st) {
+    decode_advance_kernel<<<(std::max(n, 1) + 127) / 128, 128, 0, st>>>(n, ct, beg, tout, ints, ctl, ring, err, ring_err);
+    WM_CHECK(hipGetLastError());
+}
+
 }  // namespace wm
