@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
 // the chip (160 -> 320 at 128 clips); every output is bit-identical to TOK = 16 (each MFMA output row
 // is its own dot product; the final sum keeps the wave order, hi before lo).
 // m is in log2 units (the step kernel scales scores by log2 e).
-template <typename T, int TOK>
+template <typename T, int TOK, int PF, bool EARLYW>
 __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restrict__ opart, const float* __restrict__ ml,
                                                             int splits, const T* __restrict__ wv, const float* __restrict__ bv,
                                                             int n, int d, int H, T* __restrict__ out) {
@@ -387,39 +387,56 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
     float* wgt = (float*)(lds + RT * DMAX * 2);  // [TOK tokens][16 splits]
     static_assert(8 * RT * 64 * 4 <= RT * DMAX * 2, "reduce image fits the A image");
     auto slot_of = [&](int row, int ch) { return row * d + ((ch & ~15) | ((ch & 15) ^ (row & 15))) * 8; };
+    // the split weights: every split's (m, l) loaded at once (one memory round trip), then the
+    // reductions in split order
     if (tid < TOK) {
         const int i = i0 + tid;
         if (i < n) {
             const float* p = ml + ((long)i * splits * H + h) * 2;
+            float2 q[16];
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                if (s < splits) q[s] = *(const float2*)(p + (long)s * H * 2);
             float M = -INFINITY;
-            for (int s = 0; s < splits; s++) M = fmaxf(M, p[(long)s * H * 2]);
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                if (s < splits) M = fmaxf(M, q[s].x);
             float L = 0.0f;
-            for (int s = 0; s < splits; s++) L += __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * p[(long)s * H * 2 + 1];
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                if (s < splits) L += __builtin_amdgcn_exp2f(q[s].x - M) * q[s].y;
             const float inv = 1.0f / L;
-            for (int s = 0; s < splits; s++) wgt[tid * 16 + s] = __builtin_amdgcn_exp2f(p[(long)s * H * 2] - M) * inv;
+#pragma unroll
+            for (int s = 0; s < 16; s++)
+                if (s < splits) wgt[tid * 16 + s] = __builtin_amdgcn_exp2f(q[s].x - M) * inv;
         } else {
             for (int s = 0; s < splits; s++) wgt[tid * 16 + s] = 0.0f;
         }
     }
     // Wv fragments of this wave's k-steps (w, w+8, ...; d <= 1280 gives at most 5), loaded before
-    // phase A so their L2 latency overlaps the partial-O reads
+    // phase A so their L2 latency overlaps the partial-O reads (loading them after phase A fits two
+    // workgroups per CU but spills: 19.4 vs 18.2 us at 128 clips)
     constexpr int KMAX = DMAX / 256;
     const int r16 = lane & 15, kq = lane >> 4;
     FT bfp[KMAX][4];
+    auto load_wv = [&]() {
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
-        const int ks = wave + 8 * k;
-        if (ks < d / 32) {
+        for (int k = 0; k < KMAX; k++) {
+            const int ks = wave + 8 * k;
+            if (ks < d / 32) {
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                bfp[k][j] = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + ks * 32 + 8 * kq));
+                for (int j = 0; j < 4; j++)
+                    bfp[k][j] = __builtin_bit_cast(FT, *(const u32x4*)(wv + ((long)h * 64 + j * 16 + r16) * d + ks * 32 + 8 * kq));
+            }
         }
-    }
-    __syncthreads();
-    // the partial sums of all NE chunks of a split in flight at once (split order per element kept)
+    };
+    if constexpr (EARLYW) load_wv();
+    // the partial sums: NE chunks per split, PF splits in flight (the first PF go out with the weight
+    // and Wv loads, before the barrier; a slot is reloaded with split s + PF once split s is summed);
+    // split order per element kept
     const int q4 = d / 4;
     constexpr int NE = (TOK * (DMAX / 4) + 511) / 512;
-    float4 a[NE];
+    float4 a[NE], x[PF][NE];
     const float* src[NE];
 #pragma unroll
     for (int j = 0; j < NE; j++) {
@@ -428,15 +445,28 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         const int t = e / q4, c = (e - t * q4) * 4;
         src[j] = opart + ((long)min(i0 + t, n - 1) * splits * H + h) * d + c;
     }
-    for (int s = 0; s < splits; s++) {
-        float4 x[NE];
 #pragma unroll
-        for (int j = 0; j < NE; j++) x[j] = *(const float4*)(src[j] + (long)s * H * d);
+    for (int u = 0; u < PF; u++)
+        if (u < splits) {
 #pragma unroll
-        for (int j = 0; j < NE; j++) {
-            const int t = min(tid + 512 * j, TOK * q4 - 1) / q4;
-            const float w = wgt[t * 16 + s];
-            a[j].x += w * x[j].x; a[j].y += w * x[j].y; a[j].z += w * x[j].z; a[j].w += w * x[j].w;
+            for (int j = 0; j < NE; j++) x[u][j] = *(const float4*)(src[j] + (long)u * H * d);
+        }
+    __syncthreads();
+    for (int s0 = 0; s0 < splits; s0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int s = s0 + u;
+            if (s >= splits) break;
+#pragma unroll
+            for (int j = 0; j < NE; j++) {
+                const int t = min(tid + 512 * j, TOK * q4 - 1) / q4;
+                const float w = wgt[t * 16 + s];
+                a[j].x += w * x[u][j].x; a[j].y += w * x[u][j].y; a[j].z += w * x[u][j].z; a[j].w += w * x[u][j].w;
+            }
+            if (s + PF < splits) {
+#pragma unroll
+                for (int j = 0; j < NE; j++) x[u][j] = *(const float4*)(src[j] + (long)(s + PF) * H * d);
+            }
         }
     }
 #pragma unroll
@@ -455,6 +485,7 @@ __global__ void __launch_bounds__(512) xattn_combine_kernel(const float* __restr
         *(uint2*)(aimg + slot_of(t, ch) + half) = *(const uint2*)hi;
         *(uint2*)(aimg + slot_of(TOK + t, ch) + half) = *(const uint2*)lo;
     }
+    if constexpr (!EARLYW) load_wv();
     __syncthreads();
     f32x4 acc[NA][4];
 #pragma unroll
@@ -542,13 +573,31 @@ void launch_xattn_combine(DType dt, const float* opart, const float* ml, int spl
                           int d, int H, void* out, hipStream_t st) {
     if (n <= 0) return;
     if (splits > 16 || d % 128 || d > 1280) WM_FAIL("combine shape not supported");
-    // 8 tokens per workgroup: twice the round-2 grid (16; the same bits), 64-clip shard 2174-2190 ->
-    // 2318-2324 audio-s/s, neutral at 128 clips (profiles/r03_xcomb_tok_ab.txt)
-    dim3 grid(H, cdiv(n, 8));
-    if (dt == DType::F16)
-        xattn_combine_kernel<half_t, 8><<<grid, 512, 0, st>>>(opart, ml, splits, (const half_t*)wv, bv, n, d, H, (half_t*)out);
-    else
-        xattn_combine_kernel<bf16_t, 8><<<grid, 512, 0, st>>>(opart, ml, splits, (const bf16_t*)wv, bv, n, d, H, (bf16_t*)out);
+    // Tokens per workgroup: the largest of 16 / 8 / 4 that still gives >= 160 workgroups, else 4. Every
+    // choice gives the same bits (each MFMA output row is its own dot product; the final sum keeps the wave
+    // order). The Wv fragments are fetched once per workgroup, so fewer tokens per workgroup re-read Wv
+    // more: large-v3 (tools/xattn_tune.py, rocprofv3 trace, profiles/r05_xcomb_tok.txt) 128 clips 18.7 us
+    // at 8 tokens (320 workgroups, one per CU: two rounds) -> 13.0 at 16; 64 clips 11.0 at 8 (13.5 at 16);
+    // 16 clips 12.1 at 4 (15.2 at 8). At 16 tokens the Wv fragments are loaded after the partial sums
+    // (171 VGPRs; before them, 256 and spills: 15.1 us). Two splits' loads in flight at 4 and 8 tokens.
+    static const int tok_env = getenv("WHISPER_MI355X_XCOMB_TOK") ? atoi(getenv("WHISPER_MI355X_XCOMB_TOK")) : 0;
+    int tok = 4;
+    for (int t : {16, 8})
+        if (H * cdiv(n, t) >= 160) { tok = t; break; }
+    if (tok_env == 4 || tok_env == 8 || tok_env == 16) tok = tok_env;
+    const dim3 grid(H, cdiv(n, tok));
+#define WM_XCOMB(T_, TOK_, PF_, E_) xattn_combine_kernel<T_, TOK_, PF_, E_><<<grid, 512, 0, st>>>(opart, ml, splits, (const T_*)wv, bv, n, d, H, (T_*)out)
+#define WM_XCOMB_T(T_)                              \
+    if (tok == 4) WM_XCOMB(T_, 4, 2, true);         \
+    else if (tok == 16) WM_XCOMB(T_, 16, 1, false); \
+    else WM_XCOMB(T_, 8, 2, true);
+    if (dt == DType::F16) {
+        WM_XCOMB_T(half_t)
+    } else {
+        WM_XCOMB_T(bf16_t)
+    }
+#undef WM_XCOMB_T
+#undef WM_XCOMB
 }
 
 }  // namespace wm

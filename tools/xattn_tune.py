@@ -32,7 +32,11 @@ for n in [int(x) for x in os.environ.get("NS", "128,64").split(",")]:
         ms = C.c_float()
         assert L.whisper_mi355x_debug_xattn(ctx.ptr, *[C.c_void_p(p) for p in ptrs], n, Tn, d, 64 ** -0.25, sp, 8.0,
                                             C.c_void_p(po), 20, C.byref(ms)) == 0
+        out = np.zeros(n * d, np.uint16)
+        L.whisper_mi355x_memcpy(ctx.ptr, out.ctypes.data, C.c_void_p(po), out.nbytes, 2)
+        import hashlib
         print(f"n={n} d={d} splits={sp} {ms.value * 1e3:.1f} us per call "
-              f"(qproj+step+combine), E {n * Tn * d * 2 / (ms.value * 1e-3) / 1e9:.0f} GB/s (whole call)", flush=True)
+              f"(qproj+step+combine), E {n * Tn * d * 2 / (ms.value * 1e-3) / 1e9:.0f} GB/s (whole call) "
+              f"out {hashlib.sha1(out.tobytes()).hexdigest()[:12]}", flush=True)
     for p in ptrs + [po]:
         L.whisper_mi355x_dev_free(ctx.ptr, C.c_void_p(p))
