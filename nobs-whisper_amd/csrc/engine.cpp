@@ -1245,7 +1245,7 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
         g.slab_wt = 1;
         KT kt(s, KCLS, 2.0 * g.N * g.K + 2.0 * g.M * g.K + 4.0 * g.M * g.N, st);
         const int splits = launch_gemm_partials(dt, g, st);
-        if (splits <= 0) WM_FAIL("decode partials GEMM not applicable");
+        if (splits <= 0 || splits > 16) WM_FAIL("decode partials GEMM not applicable (splits %d)", splits);
         return DecSlabs{v.splitk, splits, (long)n_tok * N, N, bias, scale};
     };
     for (int l = 0; l < L; l++) {

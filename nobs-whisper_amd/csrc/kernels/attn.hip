@@ -564,8 +564,13 @@ __device__ __forceinline__ void attn_dec_body(const T* __restrict__ q, int q_str
     if constexpr (FQ) {
         if (tid < 64) {
             const float* p = sl.ws + (long)i * sl.ld + h * 64 + tid;
-            float v = 0.0f;
-            for (int z = 0; z < sl.splits; z++) v += p[z * sl.zstride];
+            float pz[16], v = 0.0f;  // every split's load at once (one round trip), summed in split order
+#pragma unroll
+            for (int z = 0; z < 16; z++)
+                if (z < sl.splits) pz[z] = p[z * sl.zstride];
+#pragma unroll
+            for (int z = 0; z < 16; z++)
+                if (z < sl.splits) v += pz[z];
             if (sl.bias) v = v + sl.bias[h * 64 + tid];
             red[tid] = (float)(T)(v * sl.scale);
         }
@@ -730,14 +735,26 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
     T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
     {
+        // every split's q, k, v partials loaded at once (one memory round trip; <= 16 splits), summed in
+        // split order
         const float* p = sl.ws + (long)i * sl.ld + h * 64 + lane;
+        float pq[16], pk[16], pv[16];
+#pragma unroll
+        for (int z = 0; z < 16; z++)
+            if (z < sl.splits) {
+                const float* pz = p + z * sl.zstride;
+                pq[z] = pz[0];
+                pk[z] = pz[d];
+                pv[z] = pz[2 * d];
+            }
         float vq = 0.0f, vk = 0.0f, vv = 0.0f;
-        for (int z = 0; z < sl.splits; z++) {
-            const float* pz = p + z * sl.zstride;
-            vq += pz[0];
-            vk += pz[d];
-            vv += pz[2 * d];
-        }
+#pragma unroll
+        for (int z = 0; z < 16; z++)
+            if (z < sl.splits) {
+                vq += pq[z];
+                vk += pk[z];
+                vv += pv[z];
+            }
         if (sl.bias) {
             vq = vq + sl.bias[h * 64 + lane];
             vk = vk + sl.bias[d + h * 64 + lane];
@@ -754,7 +771,9 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     float qv[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
-    constexpr int U = 8;
+    // 16 rows in flight per lane group: one pass of 128 keys per round trip (a row's score and its place
+    // in each lane group's P.V order do not depend on U)
+    constexpr int U = 16;
     const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
     for (int t0 = grp; t0 < pos; t0 += 8 * U) {
@@ -787,6 +806,14 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
         if (lane == 0) sc[w][pos] = a;
         lmax = fmaxf(lmax, a);
     }
+    // the first V chunk's loads go out before the softmax (they do not depend on P)
+    u32x4 vraw[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int t = grp + 8 * u;
+        const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
+        vraw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+    }
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
     __syncthreads();
     const int n_kv = pos + 1;
@@ -804,17 +831,18 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
 #pragma unroll
     for (int e = 0; e < 8; e++) acc[e] = 0.0f;
     for (int t0 = grp; t0 < pos; t0 += 8 * U) {
-        u32x4 raw[U];
+        if (t0 != grp) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 8 * u;
-            const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
-            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+            for (int u = 0; u < U; u++) {
+                const int t = t0 + 8 * u;
+                const u32x4* src = (const u32x4*)(V + (long)t * 64 + lane8 * 8);
+                vraw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;
-            const T* ve = (const T*)&raw[u];
+            const T* ve = (const T*)&vraw[u];
             const float p = t < pos ? sc[w][t] : 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; e++) acc[e] += p * (float)ve[e];

@@ -1156,10 +1156,22 @@ __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
         const long total4 = total >> 2;
         for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (splits <= 16) {  // every split's load at once (one round trip), summed in split order
+                float4 w[16];
+#pragma unroll
+                for (int z = 0; z < 16; z++)
+                    if (z < splits) w[z] = ((const float4*)(g.splitk_ws + z * total))[i];
+#pragma unroll
+                for (int z = 0; z < 16; z++)
+                    if (z < splits) {
+                        v.x += w[z].x; v.y += w[z].y; v.z += w[z].z; v.w += w[z].w;
+                    }
+            } else {
 #pragma unroll 4
-            for (int z = 0; z < splits; z++) {
-                const float4 w = ((const float4*)(g.splitk_ws + z * total))[i];
-                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+                for (int z = 0; z < splits; z++) {
+                    const float4 w = ((const float4*)(g.splitk_ws + z * total))[i];
+                    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+                }
             }
             const int m = (int)((i * 4) / g.N), n = (int)((i * 4) % g.N);
             epilogue<EPI, T>(g, m, n, v.x);
@@ -1224,17 +1236,26 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
     const int n = tid * 4;
     const bool on = n < g.N;
     float x[4] = {0.f, 0.f, 0.f, 0.f};
+    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = w4;
     if (on) {
+        // every load of the row goes out at once (splits <= 16, the residual, bias and LN parameters):
+        // one memory round trip; the sums keep the split order
         const float* w = g.splitk_ws + (long)m * g.N + n;
-#pragma unroll 8
-        for (int z = 0; z < splits; z++) {
-            const float4 p = *(const float4*)(w + z * total);
-            x[0] += p.x; x[1] += p.y; x[2] += p.z; x[3] += p.w;
-        }
+        float4 p[16];
+#pragma unroll
+        for (int z = 0; z < 16; z++)
+            if (z < splits) p[z] = *(const float4*)(w + z * total);
         float4* xr = (float4*)((float*)g.out + (long)m * g.ldo + n);
         const float4 r = *xr;
+        const float4 b = g.bias ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        w4 = *(const float4*)(g.ln_w + n);
+        b4 = *(const float4*)(g.ln_b + n);
+#pragma unroll
+        for (int z = 0; z < 16; z++)
+            if (z < splits) {
+                x[0] += p[z].x; x[1] += p[z].y; x[2] += p[z].z; x[3] += p[z].w;
+            }
         if (g.bias) {
-            const float4 b = *(const float4*)(g.bias + n);
             x[0] = x[0] + b.x; x[1] = x[1] + b.y; x[2] = x[2] + b.z; x[3] = x[3] + b.w;
         }
         x[0] = x[0] + r.x; x[1] = x[1] + r.y; x[2] = x[2] + r.z; x[3] = x[3] + r.w;
@@ -1263,8 +1284,6 @@ __global__ void __launch_bounds__(1024) splitk_reduce_resid_ln4_kernel(const Gem
     const float variance = (float)(s2 / g.N);
     const float scale = 1.0f / sqrtf(variance + 1e-5f);
     if (!on) return;
-    const float4 w4 = *(const float4*)(g.ln_w + n);
-    const float4 b4 = *(const float4*)(g.ln_b + n);
     const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
     T y[4];
 #pragma unroll
@@ -1627,7 +1646,7 @@ static int dec_splits_for(int tiles, int nk) {
 
 template <typename T>
 static void launch_reduce_resid_ln(const GemmArgs& g, int splits, hipStream_t st) {
-    if (g.N % 4 == 0 && g.N <= 4096) {
+    if (g.N % 4 == 0 && g.N <= 4096 && splits <= 16) {
         const int threads = cdiv(g.N / 4, 64) * 64;
         splitk_reduce_resid_ln4_kernel<T><<<g.M, threads, 0, st>>>(g, splits);
         return;
