@@ -1156,22 +1156,10 @@ __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
         const long total4 = total >> 2;
         for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (splits <= 16) {  // every split's load at once (one round trip), summed in split order
-                float4 w[16];
-#pragma unroll
-                for (int z = 0; z < 16; z++)
-                    if (z < splits) w[z] = ((const float4*)(g.splitk_ws + z * total))[i];
-#pragma unroll
-                for (int z = 0; z < 16; z++)
-                    if (z < splits) {
-                        v.x += w[z].x; v.y += w[z].y; v.z += w[z].z; v.w += w[z].w;
-                    }
-            } else {
 #pragma unroll 4
-                for (int z = 0; z < splits; z++) {
-                    const float4 w = ((const float4*)(g.splitk_ws + z * total))[i];
-                    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
-                }
+            for (int z = 0; z < splits; z++) {
+                const float4 w = ((const float4*)(g.splitk_ws + z * total))[i];
+                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
             }
             const int m = (int)((i * 4) / g.N), n = (int)((i * 4) % g.N);
             epilogue<EPI, T>(g, m, n, v.x);
