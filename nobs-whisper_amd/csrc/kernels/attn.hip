@@ -1072,11 +1072,12 @@ void launch_attn_decode(DType dt, const void* q, int q_stride, const void* cache
 #undef WM_ATTN_DEC
 }
 
-// WHISPER_MI355X_XWIDE_MAX (default 4, read per call): decode steps of up to this many clips use the
-// 1024-thread cache-form kernel
+// WHISPER_MI355X_XWIDE_MAX (default 8, read per call): decode steps of up to this many clips use the
+// 1024-thread cache-form kernel (large-v3 bf16, profiles/r05_xwide_ab.txt: 8 clips 633 -> 664 audio-s/s
+// with it; 16 clips 1124 -> 1070 and 32 clips 1700 -> 1645 without it stays faster)
 int attn_cross_wide_max() {
     const char* e = getenv("WHISPER_MI355X_XWIDE_MAX");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 8;
 }
 
 void launch_attn_cross_step(DType dt, const DecSlabs& sl, const void* cache, const int* slot, const int* n_kv, int n,
