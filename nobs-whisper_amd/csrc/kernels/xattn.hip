@@ -91,13 +91,17 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // 16 NT tokens, K = 64. Swapped product C^T[c][tok] = Wk_h^T[c][:] . q_h[tok][:]: a lane holds 4
 // consecutive columns of one token, stored as one 8-byte hi and one 8-byte lo write. Every (MT, NT)
 // gives the same bits (one MFMA pair per 16 x 16 tile whatever the tiling).
-template <typename T, int MT, int NT>
+template <typename T, int MT, int NT, bool STG = false>
 __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ q, const T* __restrict__ wkt, int n, int d,
                                                           int H, float scale, T* __restrict__ qx) {
     typedef typename Frag<T>::type FT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c0 = blockIdx.x * 64 * MT + wave * 16 * MT, h = blockIdx.y, i0 = blockIdx.z * 16 * NT;
-    if (c0 >= d) return;  // wave-uniform
+    // STG: the hi / lo tiles of the workgroup (16 NT tokens x 64 MT columns) staged in LDS, then written as
+    // whole 16-byte chunks of each token's row (the MFMA layout gives a lane 8 bytes of 4 columns)
+    constexpr int SW = 64 * MT + 8;  // padded row of the staging image (T elements)
+    __shared__ __attribute__((aligned(16))) T simg[STG ? 2 * 16 * NT * SW : 1];
+    if (!STG && c0 >= d) return;  // wave-uniform (the launch keeps d % (64 MT) == 0 for STG)
     const u32x4 zero = {0, 0, 0, 0};
     FT af[MT][2], bq[NT][2];
 #pragma unroll
@@ -122,8 +126,6 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
 #pragma unroll
             for (int ks = 0; ks < 2; ks++) acc = mfma16x16x32(af[mt][ks], bq[nt][ks], acc);
             const int i = i0 + nt * 16 + (lane & 15);
-            if (i >= n) continue;
-            const int c = c0 + mt * 16 + 4 * (lane >> 4);
             T hi[4], lo[4];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
@@ -131,9 +133,28 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
                 hi[r] = (T)v;
                 lo[r] = (T)(v - (float)hi[r]);
             }
+            if constexpr (STG) {
+                const int tl = nt * 16 + (lane & 15), cl = wave * 16 * MT + mt * 16 + 4 * (lane >> 4);
+                *(uint2*)(simg + tl * SW + cl) = *(const uint2*)hi;
+                *(uint2*)(simg + (16 * NT + tl) * SW + cl) = *(const uint2*)lo;
+                continue;
+            }
+            if (i >= n) continue;
+            const int c = c0 + mt * 16 + 4 * (lane >> 4);
             *(uint2*)(qx + ((long)i * 2 * H + h) * d + c) = *(const uint2*)hi;
             *(uint2*)(qx + ((long)i * 2 * H + H + h) * d + c) = *(const uint2*)lo;
         }
+    if constexpr (STG) {
+        __syncthreads();
+        constexpr int CH = 64 * MT / 8, ROWS = 2 * 16 * NT;  // 16-byte chunks per row, hi + lo rows
+        const int cb = blockIdx.x * 64 * MT;
+        for (int e = threadIdx.x; e < ROWS * CH; e += 256) {
+            const int row = e / CH, ch = e - row * CH;
+            const int part = row / (16 * NT), tl = row - part * 16 * NT, i = i0 + tl;
+            if (i < n)
+                *(u32x4*)(qx + ((long)i * 2 * H + part * H + h) * d + cb + ch * 8) = *(const u32x4*)(simg + row * SW + ch * 8);
+        }
+    }
 }
 
 // ---- one pass over E per (clip, split) ------------------------------------------------------------
@@ -536,6 +557,17 @@ void launch_xattn_qproj(DType dt, const void* q, const void* wkt, int n, int d, 
     // (64 x 64; the same bits), 64-clip shard 2340-2352 vs 2314-2330 audio-s/s, 128 clips neutral
     // (profiles/r03_xcomb_tok_ab.txt)
     dim3 grid(cdiv(d, 64 * 2), H, cdiv(n, 16 * 4));
+    // staged row stores (d % 128 == 0: every model): 9.90 -> 7.81 us per large-v3 launch at 128 clips in the
+    // decode step, the same bits (profiles/r05_qproj_stg_ab.txt); WHISPER_MI355X_QPROJ_STG=0 for the 8-byte
+    // stores straight from the MFMA layout
+    static const int stg = getenv("WHISPER_MI355X_QPROJ_STG") ? atoi(getenv("WHISPER_MI355X_QPROJ_STG")) : 1;
+    if (stg && d % 128 == 0) {
+        if (dt == DType::F16)
+            xattn_qproj_kernel<half_t, 2, 4, true><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
+        else
+            xattn_qproj_kernel<bf16_t, 2, 4, true><<<grid, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)wkt, n, d, H, scale, (bf16_t*)qx);
+        return;
+    }
     if (dt == DType::F16)
         xattn_qproj_kernel<half_t, 2, 4><<<grid, 256, 0, st>>>((const half_t*)q, (const half_t*)wkt, n, d, H, scale, (half_t*)qx);
     else
