@@ -1945,9 +1945,11 @@ static void pipe_give_up(Sched& S, const std::vector<int>& act, bool upload, dou
 }
 
 // Decode the `act` jobs step after step with the next step in flight while the host processes the last one,
-// until an attempt ends (or the caller's abort callback fires); every step it ran is processed before it
-// returns, so the jobs are left exactly as the per-step path leaves them.
-static void decode_pipelined(Sched& S, const std::vector<int>& act) {
+// until an attempt ends (or the caller's abort callback fires: returns true); the jobs are left exactly as the
+// per-step path leaves them: every step it ran is processed, except the one in flight when the callback asked
+// to abort (the per-step path would not have started it). The callback is asked after every step; when an
+// attempt ended, the main loop asks it again before its next step (one call more than the per-step path).
+static bool decode_pipelined(Sched& S, const std::vector<int>& act) {
     Context* c = S.c;
     whisper_state* s = S.s;
     Workspace& w = s->ws;
@@ -1995,7 +1997,7 @@ static void decode_pipelined(Sched& S, const std::vector<int>& act) {
                 Job& j = S.jobs[act[r]];
                 if (!process_step(S, j, w.h_tout[r], nullptr)) attempt_done(S, j);
             }
-            return;
+            return false;
         }
         for (int r = 0; r < n; r++) S.jobs[act[r]].step++;
         bool ended = false;
@@ -2019,12 +2021,16 @@ static void decode_pipelined(Sched& S, const std::vector<int>& act) {
             WM_CHECK(hipMemcpyAsync(w.h_tout, w.tout, (size_t)n * sizeof(TokOut), hipMemcpyDeviceToHost, st));
             WM_CHECK(hipStreamSynchronize(st));
             kt_flush_graph(s, *G[par ^ 1]);
+            if (aborted) {
+                if (pd) *w.h_pd_err = 0;
+                return true;
+            }
             std::vector<int> still;
             for (int r = 0; r < n; r++)
                 if (S.jobs[act[r]].phase == PH_DECODE) still.push_back(r);
             if (still.empty() || step_variant(c, s, (int)still.size()) != step_variant(c, s, n)) {
                 if (pd) *w.h_pd_err = 0;  // (a discarded step's give-up is not one)
-                return;
+                return false;
             }
             if (pd && *w.h_pd_err) {
                 // its persistent launch gave up: the step again, for all n rows, from the host's inputs (the
@@ -2037,7 +2043,7 @@ static void decode_pipelined(Sched& S, const std::vector<int>& act) {
                 if (!process_step(S, j, w.h_tout[r], nullptr)) attempt_done(S, j);
             }
         }
-        return;
+        return aborted;
     }
 }
 
@@ -2330,8 +2336,9 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
             if (!act.empty() && pipe_ok(S, act)) {
                 if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
                 const double td = now_ms();
-                decode_pipelined(S, act);
+                const bool ab = decode_pipelined(S, act);
                 S.t_decode += now_ms() - td;
+                if (ab) { aborted = true; break; }
             } else if (!act.empty()) {
                 if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) { aborted = true; break; }
                 const double td = now_ms();

@@ -49,3 +49,47 @@ def test_pipelined_equals_per_step(wrs, monkeypatch, shape, n, cross, fixed, pip
     print(f"{shape} x {n} fixed {fixed}: {ntok} tokens")
     assert ntok > 0
     assert a == b
+
+
+def test_pipelined_abort_callback(wrs, monkeypatch):
+    """whisper_full's abort callback (asked before every decode step, whisper.rs passes none but the ABI has
+    it) with pipelined decoding: the call returns 0 with the windows finished before the abort, a prefix of an
+    unaborted run's segments, as on the per-step path; the state then transcribes the clip again (with the
+    aborted call's text as its prompt_past, so not the fresh result)."""
+    import ctypes as C
+    from conftest import model_path
+    monkeypatch.setenv("WHISPER_MI355X_PIPE_MIN", "2")
+    cbt = C.CFUNCTYPE(C.c_bool, C.c_void_p)
+    pcm = synthetic_pcm(5, seconds=75.0)
+
+    def run(pipe, limit):
+        monkeypatch.setenv("WHISPER_MI355X_PIPE", "1" if pipe else "0")
+        ctx = wrs.WhisperContext(model_path("base+conf"), dtype=wrs.F16)
+        st = ctx.create_state()
+        calls = [0]
+
+        def cb(_):
+            calls[0] += 1
+            return limit is not None and calls[0] >= limit
+        f = cbt(cb)
+        p = wrs.reference_full_params("en")
+        p.temperature_inc = 0.0
+        p.abort_callback = C.cast(f, C.c_void_p)
+        assert st.full(p, pcm) == 0
+        segs = [([t[0] for t in s.tokens], s.t0, s.t1, s.text)
+                for s in (st.get_segment(i) for i in range(st.full_n_segments()))]
+        p.abort_callback = None
+        assert st.full(p, pcm) == 0  # the same state, no abort: the unaborted result
+        again = [([t[0] for t in s.tokens], s.t0, s.t1, s.text)
+                 for s in (st.get_segment(i) for i in range(st.full_n_segments()))]
+        st.close()
+        ctx.close()
+        return segs, again, calls[0]
+
+    full, _, n_calls = run(True, None)
+    assert len(full) >= 2 and n_calls > 20
+    for pipe in (True, False):
+        segs, again, _ = run(pipe, n_calls // 2)
+        assert len(segs) < len(full) and segs == full[:len(segs)], (pipe, len(segs), len(full))
+        assert len(again) > 0
+    print(f"{len(full)} segments, {n_calls} callback calls unaborted")
