@@ -953,7 +953,9 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
         KT kt(s, K_PDEC, bytes, st);
         launch_pdec(c->dt, a, st);
     }
-    WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + a.gr.err_bytes, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    // (a pipelined step graph's advance kernel writes the error word to its ring slot instead)
+    if (!s->pipe_capture)
+        WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + a.gr.err_bytes, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
     tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }
@@ -1069,7 +1071,8 @@ static void decoder_rows_bdec(Context* c, whisper_state* s, const DecView& v, in
             launch_xattn_step(c->dt, w.enc, a.slot, w.qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st);
         }
     }
-    WM_CHECK(hipMemcpyAsync(w.h_pd_err, w.bd_sync + bdec_err_index(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (!s->pipe_capture)
+        WM_CHECK(hipMemcpyAsync(w.h_pd_err, w.bd_sync + bdec_err_index(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
     tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }
@@ -1772,9 +1775,11 @@ static whisper_state::DecGraph* dec_graph(Context* c, whisper_state* s, int n, i
     whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, g_pdec_gen, par, nullptr, {}};
     hipGraph_t graph;
     s->capture_ev = &g.ev;
+    s->pipe_capture = par > 0;
     WM_CHECK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
     decoder_launch(c, s, n, n, true, s->direct);
     logits_launch(c, s, n);
+    s->pipe_capture = false;
     if (par > 0) {
         Workspace& w = s->ws;
         char* slot = w.ring + (par - 1) * ring_slot_bytes(w);
@@ -2032,7 +2037,7 @@ static bool decode_pipelined(Sched& S, const std::vector<int>& act) {
                 if (pd) *w.h_pd_err = 0;  // (a discarded step's give-up is not one)
                 return false;
             }
-            if (pd && *w.h_pd_err) {
+            if (pd && *(const unsigned*)(w.h_ring + (par ^ 1) * slot_b + (size_t)w.cap_jobs * sizeof(TokOut))) {
                 // its persistent launch gave up: the step again, for all n rows, from the host's inputs (the
                 // graph's own advance has moved the device's past step k + 1)
                 pipe_give_up(S, act, true, now_ms());

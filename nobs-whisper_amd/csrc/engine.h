@@ -250,6 +250,7 @@ struct whisper_state {
     struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; int pdec; int gen; int par; hipGraphExec_t exec; std::vector<KPending> ev; };
     std::vector<DecGraph> dec_graphs;
     std::vector<KPending>* capture_ev = nullptr;  // non-null while a decode step is being captured
+    bool pipe_capture = false;  // capturing a pipelined step graph (its advance kernel copies the error word)
     double cur_self_work = 0;                     // self-attention bytes of the current step
     whisper_state* twin = nullptr;                // second half of a paired batch (full_batch)
     bool pdec_block = false;                      // re-running a step whose persistent launch gave up
