@@ -44,7 +44,8 @@ WHISPER_API int whisper_mi355x_broadcast_weights(struct whisper_context * ctx, c
  * whisper_full_with_state call on a fresh state would process it. pcm[j] points at n_samples[j]
  * f32 samples, on the host (pcm_on_device = false) or already in this context's HBM (true).
  * Fixed-work benchmark mode: fixed_tokens > 0 decodes exactly that many tokens per window with EOT
- * suppressed and no temperature fallback. Returns 0 on success. */
+ * suppressed and no temperature fallback; at most n_text_ctx / 2 - 4 (a window's limit,
+ * 220), else -1. Returns 0 on success. */
 WHISPER_API int whisper_mi355x_full_batch(struct whisper_context * ctx, struct whisper_state * state,
                                           struct whisper_full_params params, const float * const * pcm,
                                           const int * n_samples, int n_jobs, bool pcm_on_device, int fixed_tokens);
@@ -72,7 +73,6 @@ WHISPER_API long whisper_mi355x_batch_decoded_tokens(struct whisper_state * stat
 WHISPER_API long whisper_mi355x_decoded_tokens_total(void);
 /* Debug: the batched persistent decoder chain's hand-off counters and error word after the state's last
  * decode step (u32 words, out must hold them); returns the word count (-count if cap is too small). */
-WHISPER_API int whisper_mi355x_debug_bdec_sync(struct whisper_state * state, unsigned * out, int cap);
 /* Debug: device pointers of a state's decode workspace (0 residual x, 1 final LayerNorm rows, 2 q|k|v rows of
  * the batched chain, 3 attention outputs, 4 GELU rows, 5 cross q, 6 Q', 7 cross-attention partials, 8 their
  * {m, l}); NULL when not allocated. */

@@ -447,7 +447,9 @@ int whisper_mi355x_broadcast_weights(struct whisper_context* ctx, const char uid
 
 int whisper_mi355x_full_batch(struct whisper_context* ctx, struct whisper_state* s, struct whisper_full_params p,
                               const float* const* pcm, const int* n, int n_jobs, bool on_device, int fixed_tokens) {
-    if (!ctx || !s || n_jobs <= 0) return -1;
+    // fixed work decodes at most a window's n_max = n_text_ctx / 2 - 4 tokens (whisper.cpp's limit: a 229-token
+    // prompt + 220 tokens ends at the last self-cache row)
+    if (!ctx || !s || n_jobs <= 0 || fixed_tokens > ctx->c.hp.n_text_ctx / 2 - 4) return -1;
     FullOpts o;
     o.fixed_tokens = fixed_tokens;
     return guarded(s, [&] { return full_batch(&ctx->c, s, p, pcm, n, n_jobs, on_device, o, false); });
@@ -455,7 +457,8 @@ int whisper_mi355x_full_batch(struct whisper_context* ctx, struct whisper_state*
 int whisper_mi355x_full_batch_forced(struct whisper_context* ctx, struct whisper_state* s, struct whisper_full_params p,
                                      const float* const* pcm, const int* n, int n_jobs, bool on_device, int fixed_tokens,
                                      const int* forced, const int* spot, int n_spot, float* spot_logits) {
-    if (!ctx || !s || n_jobs <= 0 || fixed_tokens <= 0 || !forced || n_spot < 0 || (n_spot && (!spot || !spot_logits)))
+    if (!ctx || !s || n_jobs <= 0 || fixed_tokens <= 0 || fixed_tokens > ctx->c.hp.n_text_ctx / 2 - 4 || !forced || n_spot < 0 ||
+        (n_spot && (!spot || !spot_logits)))
         return -1;
     for (int k = 0; k < n_spot; k++)
         if (spot[k] < 0 || spot[k] >= n_jobs) return -1;
@@ -561,28 +564,18 @@ void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
 void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
 void whisper_mi355x_set_pdec_spin(long ticks) {
     wm::g_pdec_spin_ticks = ticks;
-    wm::g_pdec_gen++;
+    wm::g_pdec_gen.fetch_add(1, std::memory_order_release);
 }
 void whisper_mi355x_set_pdec_stamps(void* dev) {
     wm::g_pdec_stamps = (unsigned long long*)dev;
-    wm::g_pdec_gen++;
+    wm::g_pdec_gen.fetch_add(1, std::memory_order_release);
 }
-// debug: the batched chain's counter block of the state's last step (u32 words) -> host; returns the word count
-int whisper_mi355x_debug_bdec_sync(struct whisper_state* s, unsigned* out, int cap) {
-    if (!s || !s->ctx || !s->ws.bd_sync) return -1;
-    const int n = (int)(wm::bdec_sync_bytes(s->ctx->hp.n_text_layer) / 4);
-    if (cap < n) return -n;
-    hipSetDevice(s->device);
-    if (hipStreamSynchronize(s->stream) != hipSuccess) return -1;
-    if (hipMemcpy(out, s->ws.bd_sync, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return n;
-}
-// debug: device pointers of the state's decode workspace: 0 x (f32 [rows][d]), 1 final LN rows, 2 q|k|v rows of
-// the chain, 3 attention outputs, 4 GELU rows, 5 cross q, 6 Q', 7 cross partials, 8 their {m, l}
+// debug: device pointers of the state's decode workspace: 0 x (f32 [rows][d]), 1 final LN rows, 2 (unused), 3
+// attention outputs, 4 GELU rows, 5 cross q, 6 Q', 7 cross partials, 8 their {m, l}
 void* whisper_mi355x_debug_ws(struct whisper_state* s, int which) {
     if (!s) return nullptr;
     const wm::Workspace& w = s->ws;
-    void* p[9] = {w.dx, w.dh, w.bq, w.datt, w.dff, w.dq, w.qx, w.xo, w.xml};
+    void* p[9] = {w.dx, w.dh, nullptr, w.datt, w.dff, w.dq, w.qx, w.xo, w.xml};
     return which >= 0 && which < 9 ? p[which] : nullptr;
 }
 long whisper_mi355x_decoded_tokens_total(void) { return wm::g_decoded_tokens_total.load(); }

@@ -295,7 +295,7 @@ static void free_ws(Workspace& w) {
     dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
     dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.win_job);
     dfree(w.pcm); dfree(w.mel); dfree(w.mel_ptrs); dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo);
-    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync); dfree(w.bd_sync); dfree(w.bq); dfree(w.bhn);
+    dfree(w.xml); dfree(w.kvslot); dfree(w.hs); dfree(w.qtiles); dfree(w.wdq); dfree(w.pd_sync);
     if (w.h_pd_err) hipHostFree(w.h_pd_err);
     if (w.h_ring) hipHostFree(w.h_ring);
     for (auto& e : w.ring_ev)
@@ -385,7 +385,7 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         const int n_tok = n_jobs * (hp.n_text_ctx / 2 + 8);
         dfree(w.cross); dfree(w.self); dfree(w.dx); dfree(w.dh); dfree(w.dq); dfree(w.datt); dfree(w.dff);
         dfree(w.lrow); dfree(w.logits); dfree(w.probs); dfree(w.tok); dfree(w.ctl); dfree(w.tout); dfree(w.lrec); dfree(w.mel_ptrs);
-        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles); dfree(w.bq); dfree(w.bhn);
+        dfree(w.splitk); dfree(w.enc); dfree(w.qx); dfree(w.xo); dfree(w.xml); dfree(w.kvslot); dfree(w.qtiles);
         if (w.h_ring) { WM_CHECK(hipHostFree(w.h_ring)); w.h_ring = nullptr; w.ring = nullptr; }
         for (void** h : {(void**)&w.h_qtiles, (void**)&w.h_ints, (void**)&w.h_tout, (void**)&w.h_ctl})
             if (*h) { void* q = *h; *h = nullptr; WM_CHECK(hipHostFree(q)); }
@@ -843,11 +843,9 @@ static int pdec_max() {
 }
 
 // The per-call switches that choose a decode step's kernels, folded into the key of its captured graph.
-static bool bdec_on();
 static int dec_path_sig() {
     return small_m_max() | (std::min(std::max(quant_small_max(), 0), 1023) << 6) |
-           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26) | ((g_pdec_blocks & 1) << 29) |
-           ((bdec_on() ? 1 : 0) << 30);
+           (std::min(std::max(attn_cross_wide_max(), 0), 1023) << 16) | (pdec_max() << 26) | ((g_pdec_blocks & 1) << 29);
 }
 
 // Quantized files: the persistent step reads the context's expanded compute-type copy when it exists
@@ -956,123 +954,6 @@ static void decoder_rows_pdec(Context* c, whisper_state* s, const DecView& v) {
     // (a pipelined step graph's advance kernel writes the error word to its ring slot instead)
     if (!s->pipe_capture)
         WM_CHECK(hipMemcpyAsync(w.h_pd_err, (const char*)w.pd_sync + a.gr.err_bytes, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
-    tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
-}
-
-// The batched persistent chain (kernels/bdec.hip) for decode steps of 5..128 clips in the direct cross form:
-// per layer one chain launch around the pass over E, instead of ~16 launches (VERDICT r4 "next" #3).
-// WHISPER_MI355X_BDEC=0 turns it off (read per call). Not while another call of this process is inside
-// full_batch (a second state, the twin half of a paired batch): the chain needs its 256 workgroups resident
-// together, and two such launches on two streams could each hold half the CUs.
-std::atomic<int> g_calls_in_flight{0};
-static bool bdec_on() {
-    const char* e = getenv("WHISPER_MI355X_BDEC");
-    return e && atoi(e) != 0;  // (opt-in until it beats the launch chain at every clip count)
-}
-static bool bdec_use(Context* c, whisper_state* s, int n, bool xdirect) {
-    if (!xdirect || s->pdec_block || s->pdec_off || !bdec_on() || n < 5 || n > 128 || s->step_rows > 128) return false;
-    if (c->fp8_enc && !c->dec8.empty()) return false;
-    if (c->quant && !c->expanded.load(std::memory_order_acquire)) return false;
-    if (!bdec_supported(c->hp.n_text_state) || c->hp.n_text_state != 64 * c->hp.n_text_head) return false;
-    if (!c->w.wkT || g_calls_in_flight.load() > 1) return false;
-    static const int cus = [] {
-        int dev = 0, v = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-        return v;
-    }();
-    return cus == 256;
-}
-
-// Device array of the decoder layers' pointers for the chain (once per context)
-static const BdecLayer* bdec_layers(Context* c) {
-    std::lock_guard<std::mutex> lk(c->pdec_mu);
-    if (!c->bdec_layers) {
-        const int d = c->hp.n_text_state, H = c->hp.n_text_head;
-        std::vector<BdecLayer> h(c->hp.n_text_layer);
-        for (int l = 0; l < c->hp.n_text_layer; l++) {
-            const LayerW& L = c->w.dec[l];
-            LayerMats m{L.wqkv, L.wo, L.wxq, L.wxo, L.w1, L.w2};
-            if (c->quant) m = c->exp_dec[l];
-            BdecLayer b{};
-            b.wqkv = m.wqkv; b.wo = m.wo; b.wxq = m.wxq; b.wxo = m.wxo; b.w1 = m.w1; b.w2 = m.w2;
-            b.wv = (const char*)c->w.wkv_cross + (size_t)(2 * l + 1) * d * d * 2;
-            b.wkt = (const char*)c->w.wkT + (size_t)l * H * d * 64 * 2;
-            b.bqkv = L.bqkv; b.bo = L.bo; b.bxq = L.bxq; b.bxo = L.bxo; b.b1 = L.b1; b.b2 = L.b2;
-            b.bv = c->w.bkv_cross + (size_t)(2 * l + 1) * d;
-            b.ln1_w = L.ln1_w; b.ln1_b = L.ln1_b; b.lnx_w = L.lnx_w; b.lnx_b = L.lnx_b; b.ln2_w = L.ln2_w; b.ln2_b = L.ln2_b;
-            h[l] = b;
-        }
-        void* p = nullptr;
-        WM_CHECK(hipMalloc(&p, h.size() * sizeof(BdecLayer)));
-        WM_CHECK(hipMemcpy(p, h.data(), h.size() * sizeof(BdecLayer), hipMemcpyHostToDevice));
-        c->bdec_layers = p;
-    }
-    return (const BdecLayer*)c->bdec_layers;
-}
-
-// Everything the chain allocates, before a decode step is captured
-static void bdec_prepare(Context* c, whisper_state* s) {
-    Workspace& w = s->ws;
-    bdec_layers(c);
-    if (!w.bd_sync) dalloc(w.bd_sync, bdec_sync_bytes(c->hp.n_text_layer));
-    if (!w.bq) dalloc(w.bq, (size_t)w.cap_jobs * 3 * c->hp.n_text_state * esize(c->dt));
-    if (!w.bhn) dalloc(w.bhn, (size_t)w.cap_jobs * c->hp.n_text_state * esize(c->dt));
-    if (!w.h_pd_err) {
-        WM_CHECK(hipHostMalloc((void**)&w.h_pd_err, 16, 0));
-        *w.h_pd_err = 0;
-    }
-}
-
-// One decode step of the view's rows: the chain's launches around the passes over E, then the logits GEMM
-// (graph-capturable). The error word goes to the host as a node of the step's graph (decode_step re-runs the
-// step on the per-kernel path if a launch gave up).
-static void decoder_rows_bdec(Context* c, whisper_state* s, const DecView& v, int kt_stride) {
-    const Hparams& hp = c->hp;
-    Workspace& w = s->ws;
-    const int d = hp.n_text_state, H = hp.n_text_head, L = hp.n_text_layer, V = hp.n_vocab, n = v.n, Ta = hp.n_audio_ctx;
-    hipStream_t st = v.st;
-    if (!w.bd_sync || !w.bq || !w.bhn) WM_FAIL("bdec: buffers not allocated (bdec_prepare)");
-    const int S = xattn_splits(n, Ta);
-    BdecArgs a{};
-    a.layers = bdec_layers(c);
-    a.L = L; a.M = n; a.d = d; a.n_text_ctx = hp.n_text_ctx; a.S = S;
-    a.tok_emb = c->w.tok_emb_f32 ? (const void*)c->w.tok_emb_f32 : c->w.tok_emb;
-    a.te_f32 = c->w.tok_emb_f32 != nullptr;
-    a.pos_d = c->w.pos_d;
-    a.lnd_w = c->w.lnd_w; a.lnd_b = c->w.lnd_b;
-    a.out_dh = (char*)w.dh + (size_t)v.r0 * d * esize(c->dt);
-    a.tok = w.tok + v.r0; a.pos = w.pos + v.r0; a.slot = w.slot + v.r0;
-    a.self_cache = w.self; a.k_scale = c->k_scale;
-    a.x = w.dx + (size_t)v.r0 * d;
-    a.bq = w.bq; a.batt = w.datt; a.bff = w.dff; a.bxq = w.dq; a.qx = w.qx; a.hn = w.bhn;
-    a.opart = v.xo; a.ml = v.xml;
-    a.cnt = w.bd_sync; a.err_index = bdec_err_index(L);
-    a.spin_ticks = g_pdec_spin_ticks;
-    a.gelu_tab = gelu_table_device();
-    a.dbg_fence = getenv("WHISPER_MI355X_BDEC_FENCE") ? atoi(getenv("WHISPER_MI355X_BDEC_FENCE")) : 0;
-    a.dbg_skip = getenv("WHISPER_MI355X_BDEC_SKIP") ? atoi(getenv("WHISPER_MI355X_BDEC_SKIP")) : 0;
-    a.dbg_head_only = getenv("WHISPER_MI355X_BDEC_HEAD_ONLY") ? atoi(getenv("WHISPER_MI355X_BDEC_HEAD_ONLY")) : 0;
-    a.stamps = g_pdec_stamps;
-    WM_CHECK(hipMemsetAsync(w.bd_sync, 0, bdec_sync_bytes(L), st));
-    // weights once (14 d^2 per layer) + the rows' activations, per launch ~ one layer's worth
-    const double lbytes = 14.0 * d * d * 2 + (double)n * d * 4 * 16;
-    for (int l = -1; l < L; l++) {
-        a.la = l;
-        a.lb = l + 1;
-        {
-            KT kt(s, K_BDEC, lbytes, st);
-            launch_bdec(c->dt, a, st);
-        }
-        if (l + 1 < L) {
-            const bool kt_layer = (l + 1) % kt_stride == 0;
-            KT kt(s, K_ATTN_CROSS, (double)n * Ta * d * 2, st, kt_layer);
-            launch_xattn_step(c->dt, w.enc, a.slot, w.qx, n, Ta, d, S, kXattnThr, v.xo, v.xml, st);
-        }
-    }
-    if (!s->pipe_capture)
-        WM_CHECK(hipMemcpyAsync(w.h_pd_err, w.bd_sync + bdec_err_index(L), sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GemmArgs g = gemm_plain(a.out_dh, n, d, c->w.tok_emb, V, nullptr, w.logits + (size_t)v.r0 * V, V);
     tgemm_ws(s, K_GEMM_DEC, c->dt, EPI_F32, g, st, v.splitk, v.splitk_elems);
 }
@@ -1221,10 +1102,6 @@ static void decoder_rows(Context* c, whisper_state* s, const DecView& v, int n_r
     const int kt_stride = std::max(1, (s->ktime_mask >> 16) & 0xFF);
     if (fused && pdec_use(c, s, n_tok, xdirect)) {
         decoder_rows_pdec(c, s, v);
-        return;
-    }
-    if (fused && bdec_use(c, s, n_tok, xdirect)) {
-        decoder_rows_bdec(c, s, v, kt_stride);
         return;
     }
     // (the persistent and small-M paths embed the tokens themselves)
@@ -1747,7 +1624,6 @@ static const unsigned* pd_err_ptr(Context* c, whisper_state* s, int pd) {
     const Hparams& hp = c->hp;
     Workspace& w = s->ws;
     if (pd == 1) return (const unsigned*)((const char*)w.pd_sync + pdec_granules(hp.n_text_state, hp.n_text_layer, hp.n_text_head).err_bytes);
-    if (pd == 2) return w.bd_sync + bdec_err_index(hp.n_text_layer);
     return nullptr;
 }
 static size_t ring_slot_bytes(const Workspace& w) { return (size_t)w.cap_jobs * sizeof(TokOut) + 16; }
@@ -1758,9 +1634,12 @@ static size_t ring_slot_bytes(const Workspace& w) { return (size_t)w.cap_jobs * 
 // instances, which end with the device-side advance writing the step's results to ring slot par - 1.
 static whisper_state::DecGraph* dec_graph(Context* c, whisper_state* s, int n, int pd, int par) {
     const int sig = dec_path_sig();
+    // read once: a setter stores its value before it bumps the generation, so a graph captured below under
+    // generation `gen` holds that generation's (or a newer) stamps pointer and spin limit, and is retired later
+    const int gen = g_pdec_gen.load(std::memory_order_acquire);
     for (size_t i = 0; i < s->dec_graphs.size();) {
         auto& g = s->dec_graphs[i];
-        if (g.pdec && g.gen != g_pdec_gen) {
+        if (g.pdec && g.gen != gen) {
             hipGraphExecDestroy(g.exec);
             for (auto& e : g.ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
             s->dec_graphs.erase(s->dec_graphs.begin() + i);
@@ -1772,7 +1651,7 @@ static whisper_state::DecGraph* dec_graph(Context* c, whisper_state* s, int n, i
         if (g.n_tok == n && g.n_rows == n && g.mask == s->ktime_mask && g.direct == s->direct && g.sig == sig && g.pdec == pd &&
             g.par == par)
             return &g;
-    whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, g_pdec_gen, par, nullptr, {}};
+    whisper_state::DecGraph g{n, n, s->ktime_mask, s->direct, sig, pd, gen, par, nullptr, {}};
     hipGraph_t graph;
     s->capture_ev = &g.ev;
     s->pipe_capture = par > 0;
@@ -1794,17 +1673,40 @@ static whisper_state::DecGraph* dec_graph(Context* c, whisper_state* s, int n, i
     return &s->dec_graphs.back();
 }
 
-// persistent launches (the one-launch step, the chain) of different states of this process on one device never
-// overlap: two of them could hold half the CUs each
+// persistent launches of different states of this process on one device never overlap: two of them could hold
+// half the CUs each. A pipelined run holds its device's lock for the whole run (a step is always in flight), so
+// persistent steps of other threads on that device wait for it (documented). A caller's
+// abort callback runs under the lock; if it calls back into the library on the same device from the same thread,
+// that thread already holds the lock and does not take it again (g_pdec_held): its persistent launch then relies
+// on the launch's bounded waits (a launch whose workgroups cannot all become resident gives up and the step
+// re-runs on the per-kernel path) instead of deadlocking the thread on itself.
 static std::mutex g_pdec_run_mu[16];
+static thread_local unsigned g_pdec_held = 0;  // devices whose lock this thread holds (bit per device & 15)
+struct PdecRunLock {
+    int dev;
+    bool owns = false;
+    explicit PdecRunLock(int device, bool take = true) : dev(device & 15) {
+        if (take) lock();
+    }
+    void lock() {
+        if (owns || (g_pdec_held >> dev & 1)) return;
+        g_pdec_run_mu[dev].lock();
+        g_pdec_held |= 1u << dev;
+        owns = true;
+    }
+    ~PdecRunLock() {
+        if (!owns) return;
+        g_pdec_held &= ~(1u << dev);
+        g_pdec_run_mu[dev].unlock();
+    }
+};
 
 // the decode path of a step of n rows (and its buffers prepared)
 static int dec_path_prepare(Context* c, whisper_state* s, int n) {
     s->pdec_off = s->pdec_give_ups > 0 && now_ms() < s->pdec_off_until;
     s->step_rows = n;
-    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
-    if (pd == 1) pdec_prepare(c, s);
-    if (pd == 2) bdec_prepare(c, s);
+    const int pd = pdec_use(c, s, n, s->direct) ? 1 : 0;
+    if (pd) pdec_prepare(c, s);
     return pd;
 }
 
@@ -1828,7 +1730,7 @@ static void decode_step(Sched& S, const std::vector<int>& act, std::vector<std::
     // so two of them cannot hold half the CUs each (steps on different devices do not wait for each other)
     bool gave_up;
     {
-        std::lock_guard<std::mutex> lk(g_pdec_run_mu[c->device & 15]);
+        PdecRunLock lk(c->device);
         WM_CHECK(hipGraphLaunch(G->exec, s->stream));
         logits_finish(S, n, any, probs_rows);
         gave_up = *s->ws.h_pd_err != 0;
@@ -1892,15 +1794,17 @@ static bool pipe_ok(Sched& S, const std::vector<int>& act) {
 }
 
 // Everything about a decode step of n rows that can change a row's bits with n: the path (persistent step,
-// batched chain, small-M GEMMs, launch chain), the cache-form cross-attention kernel (the wide one up to
-// attn_cross_wide_max() rows) and the direct form's key-split count (xattn_splits). Equal keys: a row's
-// results at n and at n' rows are the same bits.
+// small-M GEMMs, launch chain), the cache-form cross-attention kernel (the wide one up to
+// attn_cross_wide_max() rows), the direct form's key-split count (xattn_splits), the logits GEMM's kernel
+// (gemm.hip launch_t: the unsplit 64-row kernel up to 64 rows, gemm_dec_kernel above) and the number of
+// 128-row groups (dec_groups). Equal keys: a row's results at n and at n' rows are the same bits.
 static long step_variant(Context* c, whisper_state* s, int n) {
-    const int pd = pdec_use(c, s, n, s->direct) ? 1 : bdec_use(c, s, n, s->direct) ? 2 : 0;
+    const int pd = pdec_use(c, s, n, s->direct) ? 1 : 0;
     const bool small = (c->quant && n <= quant_small_max()) || n <= small_m_max();
     const bool wide = !s->direct && n <= attn_cross_wide_max();
     const int sp = s->direct ? xattn_splits(n, c->hp.n_audio_ctx) : 0;
-    return pd | (long)small << 2 | (long)wide << 3 | (long)sp << 4;
+    const bool lg64 = n <= 64;
+    return pd | (long)small << 2 | (long)wide << 3 | (long)sp << 4 | (long)lg64 << 9 | (long)dec_groups(n) << 10;
 }
 
 // the host inputs of a decode step of the `act` jobs (their next token, position, slot, logits row)
@@ -1975,17 +1879,25 @@ static bool decode_pipelined(Sched& S, const std::vector<int>& act) {
     dec_graph(c, s, n, pd, 1);
     dec_graph(c, s, n, pd, 2);  // (may grow dec_graphs: the pointers are taken after both exist)
     whisper_state::DecGraph* G[2] = {dec_graph(c, s, n, pd, 1), dec_graph(c, s, n, pd, 2)};
-    std::unique_lock<std::mutex> lk(g_pdec_run_mu[c->device & 15], std::defer_lock);
-    if (pd) lk.lock();
+    PdecRunLock lk(c->device, pd != 0);
     double t_step = now_ms();
     WM_CHECK(hipGraphLaunch(G[0]->exec, st));
     WM_CHECK(hipEventRecord(w.ring_ev[0], st));
     for (int k = 0;; k++) {
         const int par = k & 1;
         char* hslot = w.h_ring + par * slot_b;
-        // step k produces token j.step + 1 of each job; a job continues past it only if j.step + 2 < n_max
-        bool more = false;
-        for (int r = 0; r < n; r++) more |= S.jobs[act[r]].step + 2 < S.n_max_steps;
+        // step k produces token j.step + 1 of each job; a job continues past it only if j.step + 2 < n_max. Step
+        // k + 1 runs for every row, also for a row whose attempt ends at step k, so it is launched only when every
+        // row's next position fits the self cache and the positional table (prompt + step + 1 < n_text_ctx: a
+        // 229-token prompt at the 220-token limit would write row 448); otherwise the main loop's
+        // per-step path decodes the rows that continue
+        bool more = false, fits = true;
+        for (int r = 0; r < n; r++) {
+            const Job& j = S.jobs[act[r]];
+            more |= j.step + 2 < S.n_max_steps;
+            fits &= (int)j.prompt.size() + j.step + 1 < c->hp.n_text_ctx;
+        }
+        more = more && fits;
         if (more) {
             WM_CHECK(hipGraphLaunch(G[par ^ 1]->exec, st));
             WM_CHECK(hipEventRecord(w.ring_ev[par ^ 1], st));
@@ -2153,10 +2065,6 @@ static int full_batch_one(Context* c, whisper_state* s, const whisper_full_param
         warned = true;
     }
     ensure_expanded(c, s->stream);  // quantized files: before anything is captured
-    struct InFlight {  // calls of this process inside full_batch (bdec_use)
-        InFlight() { g_calls_in_flight++; }
-        ~InFlight() { g_calls_in_flight--; }
-    } in_flight;
     Sched S;
     S.c = c; S.s = s; S.p = p; S.o = o; S.single_api = single_api;
     const Vocab& v = c->vocab;

@@ -115,7 +115,6 @@ struct Context {
     std::mutex pdec_mu;
     void* pdec_layers = nullptr;
     void* pdec_layers_exp = nullptr;  // (a quantized file's expanded copy)
-    void* bdec_layers = nullptr;      // the batched chain's layer descriptors (kernels/bdec.hip)
     // States released by whisper_free_state, kept with their workspace and captured decode graphs
     // for the next whisper_init_state: whisper.rs:83-85 creates (and drops) a state on every
     // transcribe call, which would otherwise pay ~30 hipMallocs and a graph capture per call.
@@ -179,10 +178,6 @@ struct Workspace {
     char* ring = nullptr;
     char* h_ring = nullptr;
     hipEvent_t ring_ev[2] = {nullptr, nullptr};
-    // batched persistent chain (kernels/bdec.hip): its counters + error word, and the q|k|v rows [cap][3d]
-    unsigned* bd_sync = nullptr;
-    void* bq = nullptr;
-    void* bhn = nullptr;  // the chain's LayerNorm rows [cap_jobs][d] (T)
     // mel / pcm
     float* pcm = nullptr;
     float* mel = nullptr;
@@ -202,7 +197,7 @@ struct Job;
 
 // Live per-kernel-class timing with HIP events on the state's stream (bench.py's roofline leg).
 // `work` is the algorithmic FLOPs (MFMA-bound classes) or HBM bytes (HBM-bound classes).
-enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_PDEC, K_BDEC, K_OTHER, K_NCLASS };
+enum KClass { K_GEMM_ENC = 0, K_ATTN_ENC, K_ATTN_CROSS, K_ATTN_SELF, K_GEMM_DEC, K_LOGITS, K_MEL, K_PDEC, K_OTHER, K_NCLASS };
 struct KStat { double ms = 0, work = 0; long count = 0; };
 
 }  // namespace wm
@@ -244,7 +239,7 @@ struct whisper_state {
     // changed setting never replays a graph captured for another path
     // (gen: g_pdec_gen when a persistent step was captured; its graph holds the stamps pointer and spin limit of
     // that time, so a setter call retires it)
-    // pdec: 0 = launch chain, 1 = the persistent step (kernels/pdec.hip), 2 = the batched chain (kernels/bdec.hip)
+    // pdec: 0 = launch chain, 1 = the persistent step (kernels/pdec.hip)
     // (par: 0 for the per-step path; the pipelined path alternates two instances, 0 and 1, so that one step's
     // graph events are read while the other instance runs)
     struct DecGraph { int n_tok, n_rows, mask; bool direct; int sig; int pdec; int gen; int par; hipGraphExec_t exec; std::vector<KPending> ev; };

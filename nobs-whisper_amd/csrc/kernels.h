@@ -252,7 +252,7 @@ struct PdecArgs {
 extern unsigned long long* g_pdec_stamps;
 // bumped by the stamps / spin setters: decode graphs captured with a persistent step under an older value
 // are retired, not replayed (they hold the old pointer and limit as kernel arguments)
-extern int g_pdec_gen;
+extern std::atomic<int> g_pdec_gen;  // bumped by the stamps / spin setters (capi.cpp); read once per dec_graph
 // persistent launches that gave up, every state of the process (whisper_mi355x_pdec_give_ups(NULL))
 extern std::atomic<long> g_pdec_give_ups_total;
 // 5,000,000 = 50 ms; a test hook sets 0 to make every launch give up (the re-run path)
@@ -265,47 +265,6 @@ bool pdec_supported(int d, int H, bool quant);
 int pdec_cross_splits(int H, int rows);  // key splits per (clip, head): a function of the shape only
 void launch_pdec(DType dt, const PdecArgs& a, hipStream_t st);
 const uint16_t* gelu_table_device();
-
-// ---- batched persistent decoder chain (kernels/bdec.hip) ------------------------------------------------
-// Decode steps of 5..128 clips in the direct cross form: per layer, everything but the pass over the encoder
-// output (xattn_step) runs in one 256-workgroup launch whose phases hand off by row group through counters.
-// Launch (la, lb): the tail of layer la (split merge + Wv, cross-out + residual, LN, FC1 + GELU, FC2 +
-// residual; la = -1: none, the embedding feeds layer 0) then the head of layer lb (LN, QKV with the self-cache
-// append, self attention, out-projection + residual, LN, cross-Q, the Q' projection; lb = L: the final
-// LayerNorm into out_dh instead).
-struct BdecLayer {
-    const void *wqkv, *wo, *wxq, *wxo, *w1, *w2;
-    const void* wv;   // the cross V weights of the layer [d][d] (wkv_cross + (2 l + 1) d^2)
-    const void* wkt;  // the cross K weights per head, transposed [H][d][64]
-    const float *bqkv, *bo, *bxq, *bxo, *b1, *b2, *bv;
-    const float *ln1_w, *ln1_b, *lnx_w, *lnx_b, *ln2_w, *ln2_b;
-};
-struct BdecArgs {
-    const BdecLayer* layers;  // device array [L]
-    int L, M, d, n_text_ctx, S;
-    int la, lb;
-    const void* tok_emb; int te_f32; const float* pos_d;
-    const float *lnd_w, *lnd_b; void* out_dh;
-    const int *tok, *pos, *slot;
-    void* self_cache; float k_scale;
-    float* x;                     // the residual stream [M][d] f32
-    void *bq, *batt, *bff, *bxq;  // q|k|v [M][3d], attention outputs [M][d], GELU rows [M][4d], cross q [M][d] (T)
-    void* qx;                     // Q' [M][2H][d] (T): the E pass's operand
-    void* hn;                     // LayerNorm rows [M][d] (T): the operand of QKV, cross-Q and FC1
-    const float *opart, *ml;      // the E pass's split partials [M][S][H][d], {m, l} [M][S][H][2]
-    unsigned* cnt;                // hand-off counters + error word (bdec_sync_bytes), zeroed before every step
-    int err_index;                // the error word's index in cnt (bdec_err_index)
-    long spin_ticks;
-    const uint16_t* gelu_tab;
-    int dbg_fence;                // debug (WHISPER_MI355X_BDEC_FENCE): agent release / acquire fences at every hand-off
-    int dbg_head_only;            // debug (WHISPER_MI355X_BDEC_HEAD_ONLY): launches with a layer tail do nothing
-    int dbg_skip;                 // debug (WHISPER_MI355X_BDEC_SKIP, timing only): 1 = no weight DMA, 2 = no operand loads
-    unsigned long long* stamps;   // debug (g_pdec_stamps): [L + 1 launches][3][12 phases][256 WGs] clock at input / output / operand
-};
-bool bdec_supported(int d);
-size_t bdec_sync_bytes(int L);
-int bdec_err_index(int L);
-void launch_bdec(DType dt, const BdecArgs& a, hipStream_t st);
 
 // ---- logits processing (kernels/logits.hip) ----------------------------------------------------
 struct VocabIds {

@@ -21,7 +21,7 @@ constexpr int kG = 256, kNT = 256;
 long g_pdec_spin_ticks = 5000000;
 unsigned long long* g_pdec_stamps = nullptr;
 int g_pdec_blocks = 0;
-int g_pdec_gen = 0;
+std::atomic<int> g_pdec_gen{0};
 std::atomic<long> g_pdec_give_ups_total{0};
 
 bool pdec_supported(int d, int H, bool quant) {

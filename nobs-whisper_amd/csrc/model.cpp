@@ -506,7 +506,6 @@ void free_context(Context* c) {
     if (c && c->arena_exp) { hipSetDevice(c->device); hipFree(c->arena_exp); c->arena_exp = nullptr; }
     if (c && c->pdec_layers) { hipSetDevice(c->device); hipFree(c->pdec_layers); c->pdec_layers = nullptr; }
     if (c && c->pdec_layers_exp) { hipSetDevice(c->device); hipFree(c->pdec_layers_exp); c->pdec_layers_exp = nullptr; }
-    if (c && c->bdec_layers) { hipSetDevice(c->device); hipFree(c->bdec_layers); c->bdec_layers = nullptr; }
 }
 
 }  // namespace wm

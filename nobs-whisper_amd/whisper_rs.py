@@ -172,7 +172,6 @@ def lib() -> C.CDLL:
         "whisper_mi355x_kernel_stats": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
         "whisper_mi355x_pdec_give_ups": (C.c_long, [vp]),
         "whisper_mi355x_decoded_tokens_total": (C.c_long, []),
-        "whisper_mi355x_debug_bdec_sync": (C.c_int, [vp, C.POINTER(C.c_uint), C.c_int]),
         "whisper_mi355x_debug_ws": (vp, [vp, C.c_int]),
         "whisper_mi355x_set_pdec_spin": (None, [C.c_long]),
         "whisper_mi355x_set_pdec_stamps": (None, [vp]),

@@ -108,7 +108,8 @@ def test_turbo_bf16_256_equals_two_128(wrs, monkeypatch):
     assert sum(len(b) for b in big) > 256  # every clip produced segments
 
 
-FP8_TF_TOL = 4.0   # |dlogit| bar of the teacher-forced fp8 check (the full-depth test's FP8_DEEP_TOL)
+FP8_TF_TOL = 2.5   # |dlogit| bar of the teacher-forced fp8 check (the full-depth test's FP8_DEEP_TOL; measured 0.95-0.97)
+FP8_TF_FLIP = 1.0  # argmax flips allowed only where the oracle's top-2 gap is at most this (measured up to 0.54)
 FP8_SPOT = (0, 37, 64, 101, 128, 170, 203, 255)
 N_TF = 32          # teacher-forced steps per spot clip
 
@@ -124,7 +125,7 @@ def test_turbo_fp8_b256_vs_oracle(wrs):
     (2) per clip (round 5, VERDICT r4 "next" #2): the same 256-clip call teacher-forced along the oracle's
         fixed-work greedy sequence of each spot clip (whisper_mi355x_full_batch_forced, the same kernels):
         max_v |dlogit| <= FP8_TF_TOL at every one of N_TF steps, and the argmax agrees wherever the
-        oracle's top-2 gap exceeds 2 * FP8_TF_TOL. The full 32-layer encoder depth:
+        oracle's top-2 gap exceeds FP8_TF_FLIP (round 6: both bars from round 5's measurements). The full 32-layer encoder depth:
         tests/test_gpu_fulldepth.py::test_turbo_fp8_b256_teacher_forced."""
     from conftest import model_path
     shape = "large-v3-turbo-2L+conf"
@@ -166,7 +167,7 @@ def test_turbo_fp8_b256_vs_oracle(wrs):
         flips = [(i, float(gap[i])) for i in range(N_TF) if int(np.argmax(got[i])) != int(np.argmax(ref[i]))]
         worst.append((j, round(float(per_step.max()), 3), flips))
         assert per_step.max() <= FP8_TF_TOL, (j, per_step.max(), int(per_step.argmax()))
-        assert all(g <= 2 * FP8_TF_TOL for _, g in flips), (j, flips)
+        assert all(g <= FP8_TF_FLIP for _, g in flips), (j, flips)
     print("fp8 b256 teacher-forced worst |dlogit| per spot clip (clip, worst, argmax flips):", worst)
 
 

@@ -19,17 +19,22 @@ all with the "+conf" decoders (make_model.CONF_SCALE) so windows end the way a t
     the raw logits of all 128 steps are compared with the oracle's along the same sequence:
       f16  : max_v |dlogit| / max_v |logit_oracle| <= 1e-3 at every step (the north star's bound);
       bf16 : max_v |dlogit| <= BF16_DEEP_TOL at every step, and the argmax agrees wherever the
-             oracle's top-2 gap exceeds 2 * BF16_DEEP_TOL.
+             oracle's top-2 gap exceeds BF16_FLIP_GAP.
     BF16_DEEP_TOL = 0.5 (round 5; round 4 had 2.0, fixed before its first run, and measured a worst step
     of 0.236, profiles/r04_gputests_fulldepth_v5.txt): a 2x regression of the headline dtype's decoder
-    now fails; the measured worst step is printed.
+    now fails; the measured worst step is printed. BF16_FLIP_GAP = 0.25 (round 6, VERDICT r5 weak 3: the
+    largest gap of a measured bf16 flip was 0.083; the old rule, 2 * tol = 1.0 nats, could not fail).
 (c) BASELINE configs[4]'s own workload: large-v3-turbo (32 + 4) with fp8 weights (e4m3 encoder
     GEMMs, bf16 decoder) at 256 clips in one call (two concurrent 128-clip halves, direct cross form),
     fixed work, teacher-forced like (b); 4 spot clips spread over both halves against the f16-numerics
     oracle: max_v |dlogit| <= FP8_DEEP_TOL at every step, and the argmax agrees wherever the oracle's
-    top-2 gap exceeds 2 * FP8_DEEP_TOL. FP8_DEEP_TOL = 4.0 was fixed before the first run: the reduced-
-    depth fp8 gate allows 4 nats (tests/test_gpu_batch_configs.py FP8_GAP, e4m3 moving the 2-layer
-    logits by up to ~2).
+    top-2 gap exceeds FP8_FLIP_GAP. Round 6 set both from round 5's measurements instead
+    of the bars fixed before the first run (4.0 nats, and flips allowed up to 8 nats, which could not fail):
+    FP8_DEEP_TOL 2.5 (measured worst 1.61), FP8_FLIP_GAP 1.0 (measured flips at gaps up to 0.54).
+(d) The two BASELINE workloads round 5 left without a full-depth comparison (VERDICT r5 missing 2):
+    small (12 + 12 layers, model.rs:76-86) in bf16 at 32 clips, configs[2], on the bench's default path for that
+    batch (the cross K/V cache form, the split-K launch chain); and large-v3 at 16 clips, one rank's shard of
+    configs[3] at 8 GPUs (the cache-form launch chain), f16 and bf16. Teacher-forced like (b), same bars.
 Near ties in (a) (VERDICT r4 "next" #1): the identical token prefix must reach the tie, and every segment
 that closes before it (tokens, t0, t1, text) and every window that ends before it (its decisions) must
 equal the oracle's (margin_gate.assert_closed_before_divergence).
@@ -49,7 +54,10 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 F16_REL_TOL = 1e-3
 BF16_DEEP_TOL = 0.5
-FP8_DEEP_TOL = 4.0
+BF16_FLIP_GAP = 0.25
+FP8_DEEP_TOL = 2.5
+FP8_FLIP_GAP = 1.0
+F16_FLIP_GAP = 0.05  # f16 teacher-forced logits sit within ~0.015 of the oracle's (the F16_GAP rule below)
 # (a): exact where the oracle decided every greedy step by more than F16_GAP nats, else exact up to the
 # first such near tie: the rule of every f16 whisper_full test (tests/test_gpu_pdec.py);
 # f16 teacher-forced logits sit within ~0.015 of the oracle's
@@ -127,22 +135,28 @@ def _oracle_logits(clip, shape="large-v3+conf"):
     return _oracle_fixed(shape, clip)["step_logits"].astype(np.float64)
 
 
-def _gpu_logits(wrs, dtype, shape="large-v3+conf", n_clips=N_CLIPS, spot=SPOT):
+def _gpu_logits(wrs, dtype, shape="large-v3+conf", n_clips=N_CLIPS, spot=SPOT, seeds=None, direct=True):
+    """Teacher-forced raw logits [N_TOK][len(spot)][V] of the spot positions of one n_clips call. Position j holds
+    synthetic_pcm(seeds[j]) (default j % 128); the spot positions decode the oracle sequence of their own seed,
+    the others that of a spot clip. direct: the cross form the call must have taken (the default per-call
+    choice: direct above 32 clips, the cache form up to 32)."""
     from conftest import model_path
-    key = (shape, dtype, n_clips, spot)
+    seeds = list(seeds) if seeds is not None else [j % 128 for j in range(n_clips)]
+    key = (shape, dtype, n_clips, spot, tuple(seeds))
     if key not in _GPU_LG:
-        seqs = [_oracle_seq(c % 128, shape) for c in spot]  # clip j is synthetic_pcm(j % 128)
+        seqs = [_oracle_seq(seeds[c], shape) for c in spot]
         forced = np.array([seqs[j % len(spot)] for j in range(n_clips)], np.int32)
         # the spot clips decode their own oracle sequence
         for k, c in enumerate(spot):
             forced[c] = seqs[k]
-        clips = [synthetic_pcm(k % 128) for k in range(n_clips)]
+        clips = [synthetic_pcm(s) for s in seeds]
         ctx = wrs.WhisperContext(model_path(shape), dtype=getattr(wrs, dtype))
         st = ctx.create_state()
         V = wrs.lib().whisper_n_vocab(ctx.ptr)
         rc, lg = st.full_batch_forced(wrs.reference_full_params("en"), clips, N_TOK, forced, list(spot), V)
         assert rc == 0, rc
-        assert st.info()["direct"], st.info()  # the bench's form at 128 clips (and in each 128-clip half)
+        assert st.info()["direct"] == direct, st.info()
+        assert st.pdec_give_ups() == 0
         st.close()
         ctx.close()
         _GPU_LG[key] = lg
@@ -163,10 +177,11 @@ def _check(dtype, clip, got, ref, label, model="large-v3"):
           f"argmax flips {flips}")
     if dtype == "F16":
         assert rel.max() <= F16_REL_TOL, (rel.max(), int(rel.argmax()))
+        assert all(g <= F16_FLIP_GAP for _, g in flips), flips
     else:
-        tol = FP8_DEEP_TOL if dtype == "FP8_ENC" else BF16_DEEP_TOL
+        tol, gap_bar = (FP8_DEEP_TOL, FP8_FLIP_GAP) if dtype == "FP8_ENC" else (BF16_DEEP_TOL, BF16_FLIP_GAP)
         assert per_step.max() <= tol, (per_step.max(), int(per_step.argmax()))
-        assert all(g <= 2 * tol for _, g in flips), flips
+        assert all(g <= gap_bar for _, g in flips), flips
 
 
 _FEW_LG = {}
@@ -225,3 +240,34 @@ def test_turbo_fp8_b256_teacher_forced(wrs, monkeypatch, k):
     got = _gpu_logits(wrs, "FP8_ENC", "large-v3-turbo+conf", 256, TURBO_SPOT)[:, k, :]
     _check("FP8_ENC", clip, got, ref, "b256", "large-v3-turbo")
 
+
+
+# ---- (d) configs[2] (small bf16, 32 clips) and configs[3]'s 8-GPU shard (large-v3, 16 clips), full depth -----
+SMALL_SPOT = (0, 9, 20, 31)
+
+
+@pytest.mark.parametrize("k", range(len(SMALL_SPOT)))
+def test_small_b32_bf16_teacher_forced(wrs, monkeypatch, k):
+    """BASELINE configs[2]: small (12 + 12) bf16, 32 clips in one call, the bench's default path for that batch
+    (cross K/V cache form, split-K launch chain: no persistent step above 4 clips)."""
+    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
+    clip = SMALL_SPOT[k]
+    ref = _oracle_logits(clip, "small+conf")
+    got = _gpu_logits(wrs, "BF16", "small+conf", 32, SMALL_SPOT, direct=False)[:, k, :]
+    _check("BF16", clip, got, ref, "b32", "small")
+
+
+SHARD_SEEDS = [0, 41, 86, 127] + list(range(1, 13))  # the (b) spot clips (their oracle runs are shared) + 12 more
+SHARD_SPOT = (0, 1, 2, 3)
+
+
+@pytest.mark.parametrize("dtype", ["F16", "BF16"])
+@pytest.mark.parametrize("k", range(len(SHARD_SPOT)))
+def test_largev3_b16_shard_teacher_forced(wrs, monkeypatch, dtype, k):
+    """One rank's shard of configs[3] at 8 GPUs (128 clips / 8 = 16 per rank): large-v3 at 16 clips, the cross
+    K/V cache form and its launch chain, teacher-forced along the oracle sequences of the (b) spot clips."""
+    monkeypatch.delenv("WHISPER_MI355X_CROSS", raising=False)
+    seed = SHARD_SEEDS[SHARD_SPOT[k]]
+    ref = _oracle_logits(seed)
+    got = _gpu_logits(wrs, dtype, "large-v3+conf", 16, SHARD_SPOT, seeds=SHARD_SEEDS, direct=False)[:, k, :]
+    _check(dtype, seed, got, ref, "b16 shard")

@@ -93,3 +93,54 @@ def test_pipelined_abort_callback(wrs, monkeypatch):
         assert len(segs) < len(full) and segs == full[:len(segs)], (pipe, len(segs), len(full))
         assert len(again) > 0
     print(f"{len(full)} segments, {n_calls} callback calls unaborted")
+
+
+def test_pipelined_row_at_context_end_beside_continuing_row(wrs, monkeypatch):
+    """the speculative step k + 1 runs for every row, so a row at its 220-token limit with a
+    full prompt (multilingual, no_timestamps: 1 + 224 + 4 = 229 tokens) would have been decoded at position
+    229 + 219 = 448, one past the self cache and the positional table, while another row still decoded. Here
+    clip 5 (60 s) ends its first window at step 156 (EOT: tiny+conf+eot, make_model.CONF_EOT_BOOST) and starts
+    its second while clip 1 runs its first window to the limit: the pipelined run must equal the per-step one."""
+    from conftest import model_path
+    path = model_path("tiny+conf+eot")
+    clips = [synthetic_pcm(5, seconds=60.0), synthetic_pcm(1, seconds=60.0)]
+    prompt = " ".join(f"word{k} alpha beta" for k in range(120))  # ~970 tokens: prompt_past keeps the last 224
+
+    def run(pipe):
+        monkeypatch.setenv("WHISPER_MI355X_PIPE", "1" if pipe else "0")
+        monkeypatch.setenv("WHISPER_MI355X_PIPE_MIN", "2")
+        ctx = wrs.WhisperContext(path, dtype=wrs.F16)
+        st = ctx.create_state()
+        p = wrs.reference_full_params("en")
+        p.temperature_inc = 0.0
+        p.no_timestamps = True
+        p.initial_prompt = prompt.encode()
+        assert st.full_batch(p, clips) == 0
+        out = [([([t[0] for t in s.tokens], s.t0, s.t1, s.text) for s in st.batch_segments(k)], st.decisions(k))
+               for k in range(len(clips))]
+        assert st.pdec_give_ups() == 0
+        st.close()
+        ctx.close()
+        return out
+
+    a, b = run(True), run(False)
+    # the scenario: clip 5's first window ended early (EOT), clip 1's ran to the limit (no result: failed)
+    d5, d1 = b[0][1], b[1][1]
+    print("decisions clip 5:", [(d["seek"], d["result_len0"], d["failed0"]) for d in d5],
+          "clip 1:", [(d["seek"], d["result_len0"], d["failed0"]) for d in d1])
+    assert len(d5) == 2 and 0 < d5[0]["result_len0"] < 200, d5
+    assert d1[0]["failed0"] == 1 and d1[0]["result_len0"] == 0, d1
+    assert a == b
+
+
+def test_pipelined_active_rows_cross_64(wrs, monkeypatch):
+    """when an attempt ends inside a pipelined run, the speculative step's results stand for
+    the rows still decoding only if a step of that many rows computes the same bits (step_variant). 70 clips of
+    staggered lengths in the cache form (tiny+conf: windows end on timestamps at clip-dependent steps) take the
+    active count across 64, where the logits GEMM changes kernel; results must equal the per-step path's."""
+    from conftest import model_path
+    path = model_path("tiny+conf")
+    clips = [synthetic_pcm(k % 24, seconds=10.0 + 0.5 * (k % 37)) for k in range(70)]
+    a = _run(wrs, path, clips, True, monkeypatch, cross="cache", pipe_min=2)
+    b = _run(wrs, path, clips, False, monkeypatch, cross="cache", pipe_min=2)
+    assert a == b

@@ -56,6 +56,10 @@ SHAPES = {
 # CONF_POS_SCALE x larger (the greedy sequence does not cycle, entropy stays above 2.4). With the
 # reference's FullParams the greedy t = 0 attempt then passes the fallback thresholds.
 CONF_SCALE, CONF_TS_BOOST, CONF_POS_SCALE = 6.0, 14.0, 10.0
+# "+conf+eot": the same, and the EOT row carries CONF_EOT_BOOST in column 0, so EOT competes with the top text
+# tokens and windows decoded with no_timestamps end at steps that differ from clip to clip (tests of the
+# pipelined decoding with rows at different steps, tests/test_gpu_pipe.py)
+CONF_EOT_BOOST = 18.0
 
 
 def token_beg(n_vocab: int) -> int:
@@ -227,13 +231,15 @@ def init_tensor(rng, name, shape, d, n_mels):
     return (std * rng.standard_normal(shape, dtype=np.float32)).astype(np.float32)
 
 
-def conf_adjust(name: str, t: np.ndarray, n_vocab: int) -> np.ndarray:
+def conf_adjust(name: str, t: np.ndarray, n_vocab: int, eot_boost: float = 0.0) -> np.ndarray:
     if name in ("decoder.ln.weight", "decoder.ln.bias"):
         t = t * CONF_SCALE
         t[0] = 0.0 if name.endswith("weight") else 1.0
     elif name == "decoder.token_embedding.weight":
         t[:, 0] = 0.0
         t[token_beg(n_vocab):, 0] = CONF_TS_BOOST
+        if eot_boost:
+            t[50256 + (n_vocab >= 51865), 0] = eot_boost  # token_eot (multilingual vocabularies shift it by one)
     elif name == "decoder.positional_embedding":
         t = t * CONF_POS_SCALE
     return t
@@ -361,6 +367,9 @@ def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, q
     for q in GGML_TYPES:
         if shape.endswith("+" + q):
             shape, qtype = shape[:-len(q) - 1], q
+    eot = shape.endswith("+eot")
+    if eot:
+        shape = shape[:-4]
     conf = shape.endswith("+conf")
     n_vocab, n_mels, d, h, n_enc, n_dec = SHAPES[shape[:-5] if conf else shape]
     rng = np.random.default_rng(seed)
@@ -385,7 +394,7 @@ def write_model(path: str, shape: str = "tiny", seed: int = 0, ftype: int = 1, q
                 progress(name)
             data = init_tensor(rng, name, shp, d, n_mels)
             if conf:
-                data = conf_adjust(name, data, n_vocab)
+                data = conf_adjust(name, data, n_vocab, CONF_EOT_BOOST if eot else 0.0)
             use_f16 = (ftype == 1) and not is_f32
             quant = qtype is not None and len(shp) == 2 and name not in QUANT_SKIP
             nb = name.encode()
