@@ -597,7 +597,10 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 // first read of K-tile kt+1 comes one phase later, after a barrier every issuing wave has passed
 // after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
 // slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
-template <typename T, int EPI>
+// DV (round 6 A/B): which phases of K-tile kt issue the four A pieces of K-tile kt + 1 (DV 0: all in P1; 1: two
+// in P1, two in P2; 2: all in P2; 3: one in P1, two in P2, one in P3). B of K-tile kt + 2 stays in P4 (its buffer
+// was last read in P2).
+template <typename T, int EPI, int DV = 0>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n, const int gm) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -642,6 +645,16 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
                 __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
     };
+    // pieces q0 .. q1 - 1 of stage_a (q = h * 2 + i)
+    auto stage_a_part = [&](int kt, int q0, int q1) {
+        u32x4* st = &lds[kt & 1][0];
+#pragma unroll
+        for (int q = q0; q < q1; q++)
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[q >> 1][q & 1] + kt * BK),
+                                             (lds_ptr_t)&st[((q >> 1) * 16 + wave * 2 + (q & 1)) * 64], 16, 0, 0);
+    };
+    constexpr int A1 = DV == 0 ? 4 : DV == 1 ? 2 : DV == 2 ? 0 : 1;  // pieces issued in P1
+    constexpr int A2 = DV == 0 ? 4 : DV == 1 ? 4 : DV == 2 ? 4 : 3;  // ... up to P2
     auto stage_b = [&](int kt) {
         u32x4* st = &lds[kt & 1][BM * 8];
 #pragma unroll
@@ -697,16 +710,19 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     if (wm == 1) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
+        const bool sa = kt >= 1 && kt + 1 < nk;
         // P1
         read_b(buf, 0, b0);
         read_a(buf, 0, a0);
-        if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
+        if constexpr (A1 > 0) if (sa) stage_a_part(kt + 1, 0, A1);
         mfma_q(0, 0, a0, b0);
         // P2
         read_b(buf, 1, b1);
+        if constexpr (A2 > A1) if (sa) stage_a_part(kt + 1, A1, A2);
         mfma_q(0, 1, a0, b1);
         // P3
         read_a(buf, 1, a1);
+        if constexpr (A2 < 4) if (sa) stage_a_part(kt + 1, A2, 4);
         mfma_q(1, 1, a1, b1);
         // P4: B of K-tile kt+2, then K-tile kt+1 complete (this wave's part)
         if (kt + 2 < nk) {
@@ -1680,7 +1696,15 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         const int tn = cdiv(g.N, 256);
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
-        else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn, gemm_group_m(tn));
+        else {
+            static const int dv = getenv("WHISPER_MI355X_GEMM_DV") ? atoi(getenv("WHISPER_MI355X_GEMM_DV")) : 0;
+            const int v = g_gemm_variant >= 11 && g_gemm_variant <= 13 ? g_gemm_variant - 10 : dv;
+            const int grid = tn * cdiv(g.M, 256), gm = gemm_group_m(tn);
+            if (v == 1) gemm8p_kernel<T, EPI, 1><<<grid, 512, 0, st>>>(g, tn, gm);
+            else if (v == 2) gemm8p_kernel<T, EPI, 2><<<grid, 512, 0, st>>>(g, tn, gm);
+            else if (v == 3) gemm8p_kernel<T, EPI, 3><<<grid, 512, 0, st>>>(g, tn, gm);
+            else gemm8p_kernel<T, EPI><<<grid, 512, 0, st>>>(g, tn, gm);
+        }
         return;
     }
     if ((long)g.M * g.N >= 256L * 128 * 128 && g.K % 64 == 0 && g_gemm_variant != 0) {
