@@ -135,6 +135,9 @@ WHISPER_API long whisper_mi355x_pdec_give_ups(struct whisper_state * state);
 WHISPER_API int whisper_mi355x_debug_gemm(struct whisper_context * ctx, int epi, const void * A, int M, int K,
                                           const void * B, int N, const float * bias, void * out, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_gemm_variant(int variant);
+/* debug: device buffer of [grid][4] u64 the encoder GEMM kernel fills with s_memtime stamps (entry, main loop
+ * start / end, epilogue end) per workgroup; null turns it off */
+WHISPER_API void whisper_mi355x_set_gemm_stamps(void * dev);
 /* Debug/tuning: the small-M decode GEMM (M <= 32, K % 256 == 0): out = A.B^T + bias with epilogue epi
  * (2 residual: out f32 += ..., 4 f32, 0 store, 1 gelu); with ln_w != NULL, A is f32 [M][K] and the
  * product uses LN(A) * ln_w + ln_b (K <= 1280). The first launch's result stays in out; reps more

@@ -86,7 +86,10 @@ struct GemmArgs {
     int slab_wt;
     // decode-step GEMMs in fp8 mode: B is OCP e4m3 [N][K] bytes, column n scaled by w8_scale[n]
     const float* w8_scale;
+    // debug (whisper_mi355x_set_gemm_stamps): the encoder GEMM kernel writes s_memtime at 4 points per workgroup
+    unsigned long long* stamps;
 };
+extern unsigned long long* g_gemm_stamps;
 
 void launch_gemm(DType dt, int epi, const GemmArgs& a, hipStream_t st);
 // fp8 (OCP e4m3) operands with per-row f32 scales: C = (A8 . B8^T) * a_scale[m] * b_scale[n], then

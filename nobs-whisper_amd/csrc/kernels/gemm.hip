@@ -620,6 +620,11 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         nt = r / gsz;
     }
     const int m0 = mt * BM, n0 = nt * 256;
+    // debug stamps (g.stamps): entry, main loop start, main loop end, epilogue end (shader clock), per workgroup
+    auto stamp = [&](int k) {
+        if (g.stamps && tid == 0) g.stamps[(long)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
     const T* A = (const T*)g.A;
     const T* B = (const T*)g.B;
     // DMA sources: half-tile h (rows h*128 .. +127) = 2 pieces of 8 rows x 128 B per wave
@@ -708,6 +713,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     if (wm == 1) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind
+    stamp(1);
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
         const bool sa = kt >= 1 && kt + 1 < nk;
@@ -735,6 +741,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // the barrier counts of both groups match
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp(2);
     constexpr int LDW = 68;  // padded f32 row stride of the staging image
     float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
     constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
@@ -803,6 +810,11 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             }
         }
         if (m < g.M && n < g.N) epilogue16<EPI, T, LT>(g, m, n, v, ltab);
+    }
+    if (g.stamps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(3);
     }
 }
 
@@ -1164,6 +1176,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
 // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2, 3 same,
 // pipelined, 4 256^2 phase-interleaved (the auto choice for big GEMMs)
 int g_gemm_variant = -1;
+unsigned long long* g_gemm_stamps = nullptr;
 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
@@ -1700,10 +1713,12 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             static const int dv = getenv("WHISPER_MI355X_GEMM_DV") ? atoi(getenv("WHISPER_MI355X_GEMM_DV")) : 0;
             const int v = g_gemm_variant >= 11 && g_gemm_variant <= 13 ? g_gemm_variant - 10 : dv;
             const int grid = tn * cdiv(g.M, 256), gm = gemm_group_m(tn);
-            if (v == 1) gemm8p_kernel<T, EPI, 1><<<grid, 512, 0, st>>>(g, tn, gm);
-            else if (v == 2) gemm8p_kernel<T, EPI, 2><<<grid, 512, 0, st>>>(g, tn, gm);
-            else if (v == 3) gemm8p_kernel<T, EPI, 3><<<grid, 512, 0, st>>>(g, tn, gm);
-            else gemm8p_kernel<T, EPI><<<grid, 512, 0, st>>>(g, tn, gm);
+            GemmArgs ga = g;
+            ga.stamps = g_gemm_stamps;
+            if (v == 1) gemm8p_kernel<T, EPI, 1><<<grid, 512, 0, st>>>(ga, tn, gm);
+            else if (v == 2) gemm8p_kernel<T, EPI, 2><<<grid, 512, 0, st>>>(ga, tn, gm);
+            else if (v == 3) gemm8p_kernel<T, EPI, 3><<<grid, 512, 0, st>>>(ga, tn, gm);
+            else gemm8p_kernel<T, EPI><<<grid, 512, 0, st>>>(ga, tn, gm);
         }
         return;
     }

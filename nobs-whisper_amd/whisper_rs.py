@@ -175,6 +175,7 @@ def lib() -> C.CDLL:
         "whisper_mi355x_debug_ws": (vp, [vp, C.c_int]),
         "whisper_mi355x_set_pdec_spin": (None, [C.c_long]),
         "whisper_mi355x_set_pdec_stamps": (None, [vp]),
+        "whisper_mi355x_set_gemm_stamps": (None, [vp]),
         "whisper_mi355x_set_pdec_blocks": (None, [C.c_int]),
         "whisper_mi355x_find_silence_boundaries": (C.c_int, [C.c_int, C.POINTER(vp), ip, C.c_int, C.c_int, C.c_bool,
                                                              ip, ip, C.c_int, fp, fp, C.c_int]),
