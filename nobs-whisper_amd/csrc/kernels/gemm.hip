@@ -104,9 +104,9 @@ __device__ __forceinline__ float gelu_formula(float x) {
     return x * __builtin_amdgcn_rcpf(1.0f + __expf(-u));
 }
 
-template <int EPI, typename T>
+template <int EPI, typename T, bool NOB = false>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float v) {
-    if (g.bias) v = v + g.bias[n];
+    if (!NOB && g.bias) v = v + g.bias[n];
     if constexpr (EPI == EPI_STORE) {
         if (g.sc_div > 0 && ((n / g.sc_div) % g.sc_mod) < g.sc_lim) v = v * g.scale;
         const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
@@ -145,7 +145,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, int m, int n, float 
 
 // 16 consecutive outputs of row m starting at column n (n % 16 == 0): the same math as
 // `epilogue`, with 16-byte loads/stores whenever the row segment is in bounds and aligned.
-template <int EPI, typename T, bool LTAB = false>
+// NOB: the caller has added the bias already (gemm8p_kernel loads its lane's 16 bias values once per tile)
+template <int EPI, typename T, bool LTAB = false, bool NOB = false>
 __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, float (&v)[16], lds_u16_t ltab = nullptr) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     bool vec = n + 16 <= g.N && EPI != EPI_QKV_DEC;
@@ -161,10 +162,10 @@ __device__ __forceinline__ void epilogue16(const GemmArgs& g, int m, int n, floa
     if (!vec) {
 #pragma unroll
         for (int k = 0; k < 16; k++)
-            if (n + k < g.N) epilogue<EPI, T>(g, m, n + k, v[k]);
+            if (n + k < g.N) epilogue<EPI, T, NOB>(g, m, n + k, v[k]);
         return;
     }
-    if (g.bias) {
+    if (!NOB && g.bias) {
 #pragma unroll
         for (int k = 0; k < 16; k += 4) {
             const float4 b = *(const float4*)(g.bias + n + k);
@@ -597,10 +598,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 // first read of K-tile kt+1 comes one phase later, after a barrier every issuing wave has passed
 // after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
 // slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
-// DV (round 6 A/B): which phases of K-tile kt issue the four A pieces of K-tile kt + 1 (DV 0: all in P1; 1: two
-// in P1, two in P2; 2: all in P2; 3: one in P1, two in P2, one in P3). B of K-tile kt + 2 stays in P4 (its buffer
-// was last read in P2).
-template <typename T, int EPI, int DV = 0>
+template <typename T, int EPI>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n, const int gm) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -650,16 +648,6 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
                 __builtin_amdgcn_global_load_lds((const void*)(a_src[h][i] + kt * BK),
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
     };
-    // pieces q0 .. q1 - 1 of stage_a (q = h * 2 + i)
-    auto stage_a_part = [&](int kt, int q0, int q1) {
-        u32x4* st = &lds[kt & 1][0];
-#pragma unroll
-        for (int q = q0; q < q1; q++)
-            __builtin_amdgcn_global_load_lds((const void*)(a_src[q >> 1][q & 1] + kt * BK),
-                                             (lds_ptr_t)&st[((q >> 1) * 16 + wave * 2 + (q & 1)) * 64], 16, 0, 0);
-    };
-    constexpr int A1 = DV == 0 ? 4 : DV == 1 ? 2 : DV == 2 ? 0 : 1;  // pieces issued in P1
-    constexpr int A2 = DV == 0 ? 4 : DV == 1 ? 4 : DV == 2 ? 4 : 3;  // ... up to P2
     auto stage_b = [&](int kt) {
         u32x4* st = &lds[kt & 1][BM * 8];
 #pragma unroll
@@ -716,19 +704,17 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     stamp(1);
     for (int kt = 0; kt < nk; kt++) {
         const int buf = kt & 1;
-        const bool sa = kt >= 1 && kt + 1 < nk;
-        // P1
+        // P1 (issuing the A pieces in P2, or split over P1-P3, measured the same in the engine's encode
+        // phase, profiles/r06_gemm_dv_ab.txt)
         read_b(buf, 0, b0);
         read_a(buf, 0, a0);
-        if constexpr (A1 > 0) if (sa) stage_a_part(kt + 1, 0, A1);
+        if (kt >= 1 && kt + 1 < nk) stage_a(kt + 1);
         mfma_q(0, 0, a0, b0);
         // P2
         read_b(buf, 1, b1);
-        if constexpr (A2 > A1) if (sa) stage_a_part(kt + 1, A1, A2);
         mfma_q(0, 1, a0, b1);
         // P3
         read_a(buf, 1, a1);
-        if constexpr (A2 < 4) if (sa) stage_a_part(kt + 1, A2, 4);
         mfma_q(1, 1, a1, b1);
         // P4: B of K-tile kt+2, then K-tile kt+1 complete (this wave's part)
         if (kt + 2 < nk) {
@@ -753,29 +739,50 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     }
     const lds_u16_t ltab = (lds_u16_t)(const void*)ltab_g;
     const int row = lane >> 2, c0 = (lane & 3) * 16;
-    // EPI_RESID: the residual row segment of sub-tile i + 1 is loaded while sub-tile i is staged and
-    // stored (a load -> add -> store chain per sub-tile left eight memory latencies in a row)
-    auto resid_ptr = [&](int i) -> float* {
-        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
-        float* p = (float*)g.out + (long)m * g.ldo + n;
-        return (m < g.M && n + 16 <= g.N && (((uintptr_t)p) & 15) == 0) ? p : nullptr;
-    };
-    float4 rx[4];
-    if constexpr (EPI == EPI_RESID) {
-        const float* p = resid_ptr(0);
+    const int ncol = n0 + wn * 64 + c0;  // the lane's 16 columns: the same in every sub-tile
+    // the bias of those columns, loaded once per tile (it was 4 dependent 16-byte loads per sub-tile)
+    float bia[16];
+    {
+        const bool bv = g.bias && ncol + 16 <= g.N && (((uintptr_t)(g.bias + ncol)) & 15) == 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) rx[k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 16; k += 4) {
+            const float4 b = bv ? *(const float4*)(g.bias + ncol + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            bia[k] = b.x; bia[k + 1] = b.y; bia[k + 2] = b.z; bia[k + 3] = b.w;
+        }
+        if (g.bias && !bv) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) bia[k] = ncol + k < g.N ? g.bias[ncol + k] : 0.0f;
+        }
+    }
+    // EPI_RESID: the residual row segments are read PF sub-tiles ahead (a register ring of PF x 64 bytes per
+    // lane): with one sub-tile in flight the read-modify-write of the f32 residual (512 KB per tile) ran at the
+    // latency-bound ~16 GB/s per CU and took longer than the main loop (round-6 clock stamps,
+    // tools/gemm_stamps.py: 64k cycles against 55k)
+    constexpr int PF = EPI == EPI_RESID ? 4 : 1;
+    auto resid_ptr = [&](int i) -> float* {
+        const int m = m0 + wm * 128 + i * 16 + row;
+        float* p = (float*)g.out + (long)m * g.ldo + ncol;
+        return (m < g.M && ncol + 16 <= g.N && (((uintptr_t)p) & 15) == 0) ? p : nullptr;
+    };
+    float4 rx[PF][4];
+    if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int q = 0; q < PF; q++) {
+            const float* p = resid_ptr(q);
+#pragma unroll
+            for (int k = 0; k < 4; k++) rx[q][k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         float4 cur[4];
         if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) cur[k] = rx[k];
-            if (i + 1 < 8) {
-                const float* p = resid_ptr(i + 1);
+            for (int k = 0; k < 4; k++) cur[k] = rx[i % PF][k];
+            if (i + PF < 8) {
+                const float* p = resid_ptr(i + PF);
 #pragma unroll
-                for (int k = 0; k < 4; k++) rx[k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int k = 0; k < 4; k++) rx[i % PF][k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
 #pragma unroll
@@ -792,24 +799,24 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        const int m = m0 + wm * 128 + i * 16 + row, n = n0 + wn * 64 + c0;
+        if (g.bias) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = v[k] + bia[k];
+        }
+        const int m = m0 + wm * 128 + i * 16 + row;
         if constexpr (EPI == EPI_RESID) {
             float* p = resid_ptr(i);
             if (p) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const int c = 4 * k;
-                    if (g.bias) {
-                        const float4 b = *(const float4*)(g.bias + n + c);
-                        v[c] = v[c] + b.x; v[c + 1] = v[c + 1] + b.y; v[c + 2] = v[c + 2] + b.z; v[c + 3] = v[c + 3] + b.w;
-                    }
                     ((float4*)p)[k] = make_float4(v[c] + cur[k].x, v[c + 1] + cur[k].y, v[c + 2] + cur[k].z,
                                                   v[c + 3] + cur[k].w);
                 }
                 continue;
             }
         }
-        if (m < g.M && n < g.N) epilogue16<EPI, T, LT>(g, m, n, v, ltab);
+        if (m < g.M && ncol < g.N) epilogue16<EPI, T, LT, true>(g, m, ncol, v, ltab);
     }
     if (g.stamps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1710,15 +1717,9 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         if (g_gemm_variant == 2) gemm256_kernel<T, EPI, false><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else if (g_gemm_variant == 3) gemm256_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(g, tn);
         else {
-            static const int dv = getenv("WHISPER_MI355X_GEMM_DV") ? atoi(getenv("WHISPER_MI355X_GEMM_DV")) : 0;
-            const int v = g_gemm_variant >= 11 && g_gemm_variant <= 13 ? g_gemm_variant - 10 : dv;
-            const int grid = tn * cdiv(g.M, 256), gm = gemm_group_m(tn);
             GemmArgs ga = g;
             ga.stamps = g_gemm_stamps;
-            if (v == 1) gemm8p_kernel<T, EPI, 1><<<grid, 512, 0, st>>>(ga, tn, gm);
-            else if (v == 2) gemm8p_kernel<T, EPI, 2><<<grid, 512, 0, st>>>(ga, tn, gm);
-            else if (v == 3) gemm8p_kernel<T, EPI, 3><<<grid, 512, 0, st>>>(ga, tn, gm);
-            else gemm8p_kernel<T, EPI><<<grid, 512, 0, st>>>(ga, tn, gm);
+            gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(ga, tn, gemm_group_m(tn));
         }
         return;
     }
