@@ -606,8 +606,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     __shared__ u32x4 lds[2][(BM + 256) * 8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
-    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, qx = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (qx + 1) : rr * (qx + 1) + (xcd - rr) * qx) + (orig >> 3);
     // grouped tile order (gm > 0): each group of gm m-tiles walks its m-tiles fastest, so the
     // workgroups an XCD runs at once share B (weight) tiles and a few A tiles in its L2
     int mt = wgid / tiles_n, nt = wgid % tiles_n;
@@ -738,20 +738,30 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
     const lds_u16_t ltab = (lds_u16_t)(const void*)ltab_g;
-    const int row = lane >> 2, c0 = (lane & 3) * 16;
-    const int ncol = n0 + wn * 64 + c0;  // the lane's 16 columns: the same in every sub-tile
+    // Coalesced epilogue (round 6). Lane (row = lane >> 2, q = lane & 3) of a wave's 16-row x 64-column sub-tile
+    // handles 16 of the row's columns, chosen so that each of its store instructions covers a contiguous 64-byte
+    // run of the row with its 3 neighbours: f32 outputs the columns 16 k + 4 q + (0..3), k = 0..3 (four 16-byte
+    // stores), compute-type outputs 32 h + 8 q + (0..7), h = 0..1 (two). (Sixteen consecutive columns per lane
+    // made every store instruction 64 scattered 16-byte pieces.) Arithmetic and bits are unchanged.
+    const int row = lane >> 2, q = lane & 3;
+    const int nb = n0 + wn * 64;  // the wave's 64 columns
+    constexpr bool F32O = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_GELU_POS;
+    auto colk = [&](int k) { return F32O ? nb + 16 * (k >> 2) + 4 * q + (k & 3) : nb + 32 * (k >> 3) + 8 * q + (k & 7); };
+    const bool full = nb + 64 <= g.N;  // (EPI_GELU_POS / EPI_RESID / EPI_F32 outputs are f32 rows of g.ldo floats)
     // the bias of those columns, loaded once per tile (it was 4 dependent 16-byte loads per sub-tile)
     float bia[16];
-    {
-        const bool bv = g.bias && ncol + 16 <= g.N && (((uintptr_t)(g.bias + ncol)) & 15) == 0;
 #pragma unroll
-        for (int k = 0; k < 16; k += 4) {
-            const float4 b = bv ? *(const float4*)(g.bias + ncol + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-            bia[k] = b.x; bia[k + 1] = b.y; bia[k + 2] = b.z; bia[k + 3] = b.w;
-        }
-        if (g.bias && !bv) {
+    for (int k = 0; k < 16; k++) bia[k] = 0.0f;
+    if (g.bias) {
+        if (full && (((uintptr_t)g.bias) & 15) == 0) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) bia[k] = ncol + k < g.N ? g.bias[ncol + k] : 0.0f;
+            for (int k = 0; k < 16; k += 4) {
+                const float4 b = *(const float4*)(g.bias + colk(k));
+                bia[k] = b.x; bia[k + 1] = b.y; bia[k + 2] = b.z; bia[k + 3] = b.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) bia[k] = colk(k) < g.N ? g.bias[colk(k)] : 0.0f;
         }
     }
     // EPI_RESID: the residual row segments are read PF sub-tiles ahead (a register ring of PF x 64 bytes per
@@ -761,16 +771,16 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     constexpr int PF = EPI == EPI_RESID ? 4 : 1;
     auto resid_ptr = [&](int i) -> float* {
         const int m = m0 + wm * 128 + i * 16 + row;
-        float* p = (float*)g.out + (long)m * g.ldo + ncol;
-        return (m < g.M && ncol + 16 <= g.N && (((uintptr_t)p) & 15) == 0) ? p : nullptr;
+        float* p = (float*)g.out + (long)m * g.ldo + nb + 4 * q;
+        return (m < g.M && full && (((uintptr_t)p) & 15) == 0 && (g.ldo & 3) == 0) ? p : nullptr;
     };
     float4 rx[PF][4];
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-        for (int q = 0; q < PF; q++) {
-            const float* p = resid_ptr(q);
+        for (int pq = 0; pq < PF; pq++) {
+            const float* p = resid_ptr(pq);
 #pragma unroll
-            for (int k = 0; k < 4; k++) rx[q][k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < 4; k++) rx[pq][k] = p ? *(const float4*)(p + 16 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
 #pragma unroll
@@ -782,7 +792,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             if (i + PF < 8) {
                 const float* p = resid_ptr(i + PF);
 #pragma unroll
-                for (int k = 0; k < 4; k++) rx[i % PF][k] = p ? ((const float4*)p)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int k = 0; k < 4; k++) rx[i % PF][k] = p ? *(const float4*)(p + 16 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
 #pragma unroll
@@ -794,7 +804,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         float v[16];
 #pragma unroll
         for (int k = 0; k < 16; k += 4) {
-            const float4 x = *(const float4*)(stg + row * LDW + c0 + k);
+            const float4 x = *(const float4*)(stg + row * LDW + (colk(k) - nb));
             v[k] = x.x; v[k + 1] = x.y; v[k + 2] = x.z; v[k + 3] = x.w;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -804,19 +814,81 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             for (int k = 0; k < 16; k++) v[k] = v[k] + bia[k];
         }
         const int m = m0 + wm * 128 + i * 16 + row;
+        if (m >= g.M) continue;
         if constexpr (EPI == EPI_RESID) {
             float* p = resid_ptr(i);
             if (p) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const int c = 4 * k;
-                    ((float4*)p)[k] = make_float4(v[c] + cur[k].x, v[c + 1] + cur[k].y, v[c + 2] + cur[k].z,
-                                                  v[c + 3] + cur[k].w);
+                    *(float4*)(p + 16 * k) = make_float4(v[c] + cur[k].x, v[c + 1] + cur[k].y, v[c + 2] + cur[k].z,
+                                                         v[c + 3] + cur[k].w);
+                }
+                continue;
+            }
+        } else if constexpr (EPI == EPI_F32 || EPI == EPI_GELU_POS) {
+            float* p = (float*)g.out + (long)m * g.ldo + nb + 4 * q;
+            if (full && (((uintptr_t)p) & 15) == 0 && (g.ldo & 3) == 0) {
+                const float* pp = EPI == EPI_GELU_POS ? g.pos + (long)(m % g.pos_rows) * g.N + nb + 4 * q : nullptr;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    float4 x = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+                    if constexpr (EPI == EPI_GELU_POS) {
+                        const float4 ps = *(const float4*)(pp + 16 * k);
+                        if constexpr (LT) {
+                            x.x = gelu_ltab(x.x, ltab) + ps.x; x.y = gelu_ltab(x.y, ltab) + ps.y;
+                            x.z = gelu_ltab(x.z, ltab) + ps.z; x.w = gelu_ltab(x.w, ltab) + ps.w;
+                        } else {
+                            x.x = gelu_tab(x.x) + ps.x; x.y = gelu_tab(x.y) + ps.y;
+                            x.z = gelu_tab(x.z) + ps.z; x.w = gelu_tab(x.w) + ps.w;
+                        }
+                    }
+                    *(float4*)(p + 16 * k) = x;
+                }
+                continue;
+            }
+        } else if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_F || EPI == EPI_CROSSKV) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            if (full) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int n = nb + 32 * h + 8 * q;  // 8 columns of one head (64-aligned blocks)
+                    float sc = 1.0f;
+                    T* dst;
+                    if constexpr (EPI == EPI_CROSSKV) {
+                        const int bb = m / g.ctx, t = m % g.ctx;
+                        const int l = n / (2 * g.d), kv = (n / g.d) & 1, hh = (n % g.d) >> 6, dh = n & 63;
+                        if (kv == 0) sc = g.scale;
+                        dst = (T*)g.cache + ((((long)g.row_slot[bb] * g.L + l) * 2 + kv) * g.H + hh) * g.ctx * 64 + (long)t * 64 + dh;
+                    } else {
+                        if constexpr (EPI == EPI_STORE)
+                            if (g.sc_div > 0 && ((n / g.sc_div) % g.sc_mod) < g.sc_lim) sc = g.scale;
+                        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
+                        dst = (T*)g.out + orow * g.ldo + n;
+                    }
+                    if ((((uintptr_t)dst) & 15) == 0) {
+                        T o[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            float x = v[8 * h + k];
+                            if constexpr (EPI == EPI_GELU) x = LT ? gelu_ltab(x, ltab) : gelu_tab(x);
+                            else if constexpr (EPI == EPI_GELU_F) x = gelu_formula(x);
+                            else if (sc != 1.0f) x = x * sc;
+                            o[k] = (T)x;
+                        }
+                        *(u4*)dst = *(const u4*)&o[0];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 8; k++) epilogue<EPI, T, true>(g, m, n + k, v[8 * h + k]);
+                    }
                 }
                 continue;
             }
         }
-        if (m < g.M && ncol < g.N) epilogue16<EPI, T, LT, true>(g, m, ncol, v, ltab);
+        // edge tiles (columns past N, unaligned rows): per element, the bias already added
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (colk(k) < g.N) epilogue<EPI, T, true>(g, m, colk(k), v[k]);
     }
     if (g.stamps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
