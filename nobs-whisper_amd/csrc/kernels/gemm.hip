@@ -599,161 +599,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 // after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
 // slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
 
-// The TR epilogue of gemm8p_kernel: acc[i][j][r] = C[mw + 16 i + (lane & 15)][nb + 16 j + 4 (lane >> 4) + r].
 template <typename T, int EPI>
-__device__ __forceinline__ void gemm8p_epilogue_tr(const GemmArgs& g, f32x4 (&acc)[8][4], char* lds, int tid, int mw, int nb) {
-    const int lane = tid & 63, rl = lane & 15, q = lane >> 4;
-    constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
-    if constexpr (LT) {  // the GELU table into the (now free) LDS
-        gelu_ltab_stage(lds, tid);
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    const lds_u16_t ltab = (lds_u16_t)(const void*)lds;
-    constexpr bool F32O = EPI == EPI_RESID || EPI == EPI_F32 || EPI == EPI_GELU_POS;
-    const bool full = nb + 64 <= g.N;
-    // bias of the lane's columns nb + 16 j + 4 q + r (the same in every sub-tile)
-    float bia[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) bia[j][r] = 0.0f;
-    if (g.bias) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int n = nb + 16 * j + 4 * q;
-            if (full && (((uintptr_t)g.bias) & 15) == 0) {
-                const float4 b = *(const float4*)(g.bias + n);
-                bia[j][0] = b.x; bia[j][1] = b.y; bia[j][2] = b.z; bia[j][3] = b.w;
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; r++) bia[j][r] = n + r < g.N ? g.bias[n + r] : 0.0f;
-            }
-        }
-    }
-    constexpr int PF = EPI == EPI_RESID ? 4 : 1;
-    auto rowp = [&](int i) -> float* {  // f32 outputs: row of sub-tile i at column nb + 4 q (16-byte aligned)
-        const int m = mw + 16 * i + rl;
-        float* p = (float*)g.out + (long)m * g.ldo + nb + 4 * q;
-        return (m < g.M && full && (((uintptr_t)p) & 15) == 0 && (g.ldo & 3) == 0) ? p : nullptr;
-    };
-    float4 rx[PF][4];
-    if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-        for (int pq = 0; pq < PF; pq++) {
-            const float* p = rowp(pq);
-#pragma unroll
-            for (int j = 0; j < 4; j++) rx[pq][j] = p ? *(const float4*)(p + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int m = mw + 16 * i + rl;
-        float4 cur[4];
-        if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) cur[j] = rx[i % PF][j];
-            if (i + PF < 8) {
-                const float* p = rowp(i + PF);
-#pragma unroll
-                for (int j = 0; j < 4; j++) rx[i % PF][j] = p ? *(const float4*)(p + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-        float v[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) v[j][r] = g.bias ? acc[i][j][r] + bia[j][r] : acc[i][j][r];
-        if constexpr (F32O) {
-            float* p = rowp(i);
-            if (p) {
-                const float* pp = EPI == EPI_GELU_POS ? g.pos + (long)(m % g.pos_rows) * g.N + nb + 4 * q : nullptr;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    float4 x = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
-                    if constexpr (EPI == EPI_RESID) {
-                        x.x = x.x + cur[j].x; x.y = x.y + cur[j].y; x.z = x.z + cur[j].z; x.w = x.w + cur[j].w;
-                    } else if constexpr (EPI == EPI_GELU_POS) {
-                        const float4 ps = *(const float4*)(pp + 16 * j);
-                        x.x = gelu_ltab(x.x, ltab) + ps.x; x.y = gelu_ltab(x.y, ltab) + ps.y;
-                        x.z = gelu_ltab(x.z, ltab) + ps.z; x.w = gelu_ltab(x.w, ltab) + ps.w;
-                    }
-                    *(float4*)(p + 16 * j) = x;
-                }
-                continue;
-            }
-        } else if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELU_F || EPI == EPI_CROSSKV) {
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            if (full && m < g.M) {
-                // the 64 columns share one scale (sc_div is a multiple of 64) and one head (CROSSKV)
-                float sc = 1.0f;
-                if constexpr (EPI == EPI_STORE)
-                    if (g.sc_div > 0 && ((nb / g.sc_div) % g.sc_mod) < g.sc_lim) sc = g.scale;
-                uint32_t pk[4][2];  // fragment j's 4 values as packed T pairs
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    T o[4];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        float x = v[j][r];
-                        if constexpr (EPI == EPI_GELU) x = gelu_ltab(x, ltab);
-                        else if constexpr (EPI == EPI_GELU_F) x = gelu_formula(x);
-                        else if (sc != 1.0f) x = x * sc;
-                        o[r] = (T)x;
-                    }
-                    pk[j][0] = (uint32_t)__builtin_bit_cast(uint16_t, o[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, o[1]) << 16);
-                    pk[j][1] = (uint32_t)__builtin_bit_cast(uint16_t, o[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, o[3]) << 16);
-                }
-                // fragment pair (2p, 2p + 1): the even-q lane keeps fragment 2p's columns 4q .. 4q + 3 and takes
-                // 4q + 4 .. 4q + 7 from lane + 16; the odd-q lane takes fragment 2p + 1's 4(q - 1) .. from lane - 16
-                const bool ev = (q & 1) == 0;
-                const int src = (lane ^ 16) * 4;
-#pragma unroll
-                for (int pr = 0; pr < 2; pr++) {
-                    const int j0 = 2 * pr, j1 = 2 * pr + 1;
-                    const uint32_t s0 = ev ? pk[j1][0] : pk[j0][0], s1 = ev ? pk[j1][1] : pk[j0][1];
-                    const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)s0);
-                    const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)s1);
-                    u4 w;
-                    int n;
-                    if (ev) { w = (u4){pk[j0][0], pk[j0][1], r0, r1}; n = nb + 16 * j0 + 4 * q; }
-                    else { w = (u4){r0, r1, pk[j1][0], pk[j1][1]}; n = nb + 16 * j1 + 4 * (q - 1); }
-                    T* dst;
-                    if constexpr (EPI == EPI_CROSSKV) {
-                        const int bb = m / g.ctx, t = m % g.ctx;
-                        const int l = n / (2 * g.d), kv = (n / g.d) & 1, hh = (n % g.d) >> 6, dh = n & 63;
-                        dst = (T*)g.cache + ((((long)g.row_slot[bb] * g.L + l) * 2 + kv) * g.H + hh) * g.ctx * 64 + (long)t * 64 + dh;
-                    } else {
-                        const long orow = (m / g.o_rpb) * g.o_bstride + (m % g.o_rpb) + g.o_off;
-                        dst = (T*)g.out + orow * g.ldo + n;
-                    }
-                    if ((((uintptr_t)dst) & 15) == 0) {
-                        *(u4*)dst = w;
-                    } else {
-                        const T* e = (const T*)&w;
-#pragma unroll
-                        for (int k = 0; k < 8; k++) dst[k] = e[k];
-                    }
-                }
-                continue;
-            }
-        }
-        // edge tiles: per element, the bias already added
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int n = nb + 16 * j + 4 * q + r;
-                if (n < g.N) epilogue<EPI, T, true>(g, m, n, v[j][r]);
-            }
-    }
-}
-
-// TR (round 6 A/B): the accumulators hold C^T (the MFMA operands swapped: the same products and k order, so
-// the same bits): lane l then holds 4 consecutive columns of one row per fragment, and the epilogue stores
-// straight from registers (f32 outputs: one 16-byte store per fragment; compute-type outputs: fragment pairs
-// joined across lanes l, l ^ 16 by ds_bpermute into 16-byte stores), with no LDS staging round trip.
-template <typename T, int EPI, bool TR = false>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n, const int gm) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -844,10 +690,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
 #pragma unroll
             for (int j = 0; j < 2; j++)
 #pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    if constexpr (TR) acc[mq * 4 + i][nq * 2 + j] = mfma16x16x32(bf[j][s], af[i][s], acc[mq * 4 + i][nq * 2 + j]);
-                    else acc[mq * 4 + i][nq * 2 + j] = mfma16x16x32(af[i][s], bf[j][s], acc[mq * 4 + i][nq * 2 + j]);
-                }
+                for (int s = 0; s < 2; s++) acc[mq * 4 + i][nq * 2 + j] = mfma16x16x32(af[i][s], bf[j][s], acc[mq * 4 + i][nq * 2 + j]);
         __builtin_amdgcn_s_setprio(0);
         asm volatile("s_barrier" ::: "memory");
     };
@@ -886,15 +729,6 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // the barrier counts of both groups match
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(2);
-    if constexpr (TR) {
-        gemm8p_epilogue_tr<T, EPI>(g, acc, (char*)&lds[0][0], tid, m0 + wm * 128, n0 + wn * 64);
-        if (g.stamps) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            stamp(3);
-        }
-        return;
-    }
     constexpr int LDW = 68;  // padded f32 row stride of the staging image
     float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
     constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
@@ -1958,9 +1792,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         else {
             GemmArgs ga = g;
             ga.stamps = g_gemm_stamps;
-            static const int tr = getenv("WHISPER_MI355X_GEMM_TR") ? atoi(getenv("WHISPER_MI355X_GEMM_TR")) : 0;
-            if (tr || g_gemm_variant == 14) gemm8p_kernel<T, EPI, true><<<tn * cdiv(g.M, 256), 512, 0, st>>>(ga, tn, gemm_group_m(tn));
-            else gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(ga, tn, gemm_group_m(tn));
+            gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(ga, tn, gemm_group_m(tn));
         }
         return;
     }

@@ -15,7 +15,7 @@ ctx = wrs.WhisperContext(model_path("micro"), dtype=wrs.BF16)
 rng = np.random.default_rng(0)
 d = 1280
 M = 32 * 1500
-variants = [int(v) for v in os.environ.get("DV_VARIANTS", "-1,14").split(",")]
+variants = [int(v) for v in os.environ.get("DV_VARIANTS", "-1").split(",")]
 for (N, K, name, epi) in [(3 * d, d, "qkv", 0), (d, d, "out", 2), (4 * d, d, "fc1", 7), (d, 4 * d, "fc2", 2),
                           (4 * d, d, "fc1-table", 1), (3 * d, d, "f32", 4)]:
     A = rng.standard_normal((M, K)).astype(np.float16)
