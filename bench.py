@@ -693,8 +693,8 @@ def main():
         if gd_ms > 0:
             gd = gd_w / (gd_ms * 1e-3) / 1e9
             roof["gemm_decode"] = dict(bound="hbm", achieved=round(gd, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                                       frac=round(gd / HBM_PEAK_GBS, 4), launches=int(gd_n),
-                                       avg_launch_ms=round(gd_ms / max(1, gd_n), 4), source="warm-up step, every class event-timed")
+                                       frac=round(gd / HBM_PEAK_GBS, 4), calls=int(gd_n),
+                                       avg_call_ms=round(gd_ms / max(1, gd_n), 4), source="warm-up step, every class event-timed (a call: a GEMM with its reduce kernel, or one Q-projection / split-merge launch)")
         # per-phase, time-weighted rooflines of rank 0's last step (phase clocks are host wall time
         # around stream-synchronised phases)
         pw = phase_work(args.model, nb, args.tokens, 3, form["direct"])

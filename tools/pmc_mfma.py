@@ -37,16 +37,27 @@ def main():
             if not nb or not ng:
                 continue
             b, g = busy / nb, grbm / ng
-            out[f"{tag}:{k}"] = dict(launches=nb, mfma_busy_cycles=b, grbm_gui_active=g,
-                                     mfma_busy_frac=b / (g / 8.0 * 1024.0))
+            rec = dict(launches=nb, mfma_busy_cycles=b, grbm_gui_active=g, mfma_busy_frac=b / (g / 8.0 * 1024.0))
+            # the stall counters (per dispatch; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles,
+            # MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"): shares of the waves' lifetime
+            avg = {c: v / n for c, (n, v) in cs.items() if n}
+            wc = avg.get("SQ_WAVE_CYCLES")
+            if wc:
+                for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+                    if c in avg:
+                        rec[c.lower() + "_share"] = avg[c] / wc
+            if avg.get("SQ_LDS_IDX_ACTIVE"):
+                rec["lds_bank_conflict_share"] = avg.get("SQ_LDS_BANK_CONFLICT", 0.0) / avg["SQ_LDS_IDX_ACTIVE"]
+            rec["counters"] = avg
+            out[f"{tag}:{k}"] = rec
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_mfma.json")
     for p in (path, os.path.join(ROOT, "gpurun_out", f"{tag}_pmc_mfma.json")):
         with open(p, "w") as fh:
             json.dump(out, fh, indent=1)
     for k, v in out.items():
-        print(f"{v['mfma_busy_frac']:.3f} busy  n={v['launches']}  busy={v['mfma_busy_cycles']:.3e} "
-              f"grbm={v['grbm_gui_active']:.3e}  {k[:110]}")
+        extra = "  ".join(f"{c[:-6]} {v[c]:.3f}" for c in v if c.endswith("_share"))
+        print(f"{v['mfma_busy_frac']:.3f} busy  n={v['launches']}  {extra}  {k[:100]}")
     print("wrote", path)
 
 
