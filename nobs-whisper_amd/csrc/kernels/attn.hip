@@ -734,6 +734,20 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     const long s = slot[i];
     T* K = cache + (((s * L + layer) * 2 + 0) * H + h) * (long)ctx * 64;
     T* V = cache + (((s * L + layer) * 2 + 1) * H + h) * (long)ctx * 64;
+    // the first U cached key rows of each lane group are issued before the prologue's slab loads (round 6): they
+    // do not depend on this step's q / k / v, so both land in one memory round trip (as in attn_dec_body)
+    constexpr int U = 8;
+    const u32x4 zero = {0, 0, 0, 0};
+    u32x4 raw[U];
+    auto kload = [&](int t0) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + 8 * u;
+            const u32x4* src = (const u32x4*)(K + (long)t * 64 + lane8 * 8);
+            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
+        }
+    };
+    kload(grp);
     {
         // every split's q, k, v partials loaded at once (one memory round trip; <= 16 splits), summed in
         // split order
@@ -773,17 +787,9 @@ __global__ void __launch_bounds__(64 * HPB) attn_self_step_kernel(const DecSlabs
     for (int e = 0; e < 8; e++) qv[e] = qs[w][lane8 * 8 + e];
     // 8 key rows in flight per lane group (16, with the first V chunk issued before the softmax, measured
     // 14.6 vs 13.6 us at 128 clips and 8.3 vs 8.2 at 16)
-    constexpr int U = 8;
-    const u32x4 zero = {0, 0, 0, 0};
     float lmax = -INFINITY;
     for (int t0 = grp; t0 < pos; t0 += 8 * U) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + 8 * u;
-            const u32x4* src = (const u32x4*)(K + (long)t * 64 + lane8 * 8);
-            raw[u] = t < pos ? (NT ? __builtin_nontemporal_load(src) : *src) : zero;
-        }
+        if (t0 != grp) kload(t0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int t = t0 + 8 * u;

@@ -4,6 +4,9 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_pipe.py \
+    > gpurun_out/r06_pmc_tests.txt 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/r06_pmc_tests.txt; exit 1; }
+tail -2 gpurun_out/r06_pmc_tests.txt
 bash tools/pmc_mfma.sh r06 > gpurun_out/r06_pmc_mfma.log 2>&1 || { echo "pmc rc=$?"; tail -20 gpurun_out/r06_pmc_mfma.log; exit 1; }
 cat gpurun_out/r06_pmc_mfma.log
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --variants 0 --cpu-baseline 0 --frontend 0 --app-pattern 0 --inflight-line 0 --f16-line 0 \
