@@ -1253,81 +1253,6 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         }
 }
 
-// Decode-step GEMM without split-K (round 6 experiment, g_gemm_variant 20): one workgroup = all M <= 128 rows x
-// 32 output columns over the whole K, 4 waves x 32 rows, operands loaded straight into registers (A rows are
-// each wave's own; the 32 weight rows are read by all four waves, L1-shared), DR K-chunks of 64 in flight per
-// lane. No partial slabs and no reduce launch: the epilogue runs here. The question it answers: can one CU
-// stream the M x K activations from L2 fast enough (round 2's register-direct variant could not).
-template <typename T, int EPI, int DR>
-__global__ void __launch_bounds__(256) gemm_rowfull_kernel(const GemmArgs g) {
-    typedef typename Frag<T>::type FT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n0 = blockIdx.x * 32, r0 = wave * 32;
-    const T* A = (const T*)g.A;
-    const T* B = (const T*)g.B;
-    const int nch = g.K / 64;
-    const u32x4 zero = {0, 0, 0, 0};
-    // lane: row / column (lane & 15) of each 16-row fragment, k sub-chunk (lane >> 4) * 8 of each 32-deep k-step
-    const T* ap[2];
-    const T* bp[2];
-    bool av[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const int m = r0 + i * 16 + (lane & 15);
-        av[i] = m < g.M;
-        ap[i] = A + (long)(av[i] ? m : 0) * g.a_rstride + 8 * (lane >> 4);
-        const int n = min(n0 + i * 16 + (lane & 15), g.N - 1);
-        bp[i] = B + (long)n * g.K + 8 * (lane >> 4);
-    }
-    u32x4 ra[DR][2][2], rb[DR][2][2];  // [slot][frag][k-step]
-    auto load = [&](int c, int sl) {
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int ks = 0; ks < 2; ks++) {
-                const int k = c * 64 + ks * 32;
-                ra[sl][i][ks] = av[i] ? *(const u32x4*)(ap[i] + k) : zero;
-                rb[sl][i][ks] = *(const u32x4*)(bp[i] + k);
-            }
-    };
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < DR; c++)
-        if (c < nch) load(c, c);
-    for (int c0 = 0; c0 < nch; c0 += DR) {
-#pragma unroll
-        for (int u = 0; u < DR; u++) {
-            const int c = c0 + u;
-            if (c < nch) {
-#pragma unroll
-                for (int ks = 0; ks < 2; ks++)
-#pragma unroll
-                    for (int i = 0; i < 2; i++)
-#pragma unroll
-                        for (int j = 0; j < 2; j++)
-                            acc[i][j] = mfma16x16x32(__builtin_bit_cast(FT, ra[u][i][ks]), __builtin_bit_cast(FT, rb[u][j][ks]), acc[i][j]);
-                if (c + DR < nch) load(c + DR, u);
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int n = n0 + j * 16 + (lane & 15);
-            if (n >= g.N) continue;
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int m = r0 + i * 16 + (lane >> 4) * 4 + r;
-                if (m < g.M) epilogue<EPI, T>(g, m, n, acc[i][j][r]);
-            }
-        }
-}
-
 // debug/tuning override: -1 auto, 0 register-staged, 1 LDS-DMA 128^2, 2 LDS-DMA 256^2, 3 same,
 // pipelined, 4 256^2 phase-interleaved (the auto choice for big GEMMs)
 int g_gemm_variant = -1;
@@ -1883,13 +1808,6 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
     }
     const bool fused_ln = EPI == EPI_RESID && g.ln_out != nullptr;
     const int nk = cdiv(g.K, 64);
-    if ((g_gemm_variant == 20 || g_gemm_variant == 21 || g_gemm_variant == 22) && g.M <= 128 && g.K % 64 == 0 && !fused_ln &&
-        !g.w8_scale && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_F32)) {
-        if (g_gemm_variant == 20) gemm_rowfull_kernel<T, EPI, 4><<<cdiv(g.N, 32), 256, 0, st>>>(g);
-        else if (g_gemm_variant == 21) gemm_rowfull_kernel<T, EPI, 6><<<cdiv(g.N, 32), 256, 0, st>>>(g);
-        else gemm_rowfull_kernel<T, EPI, 8><<<cdiv(g.N, 32), 256, 0, st>>>(g);
-        return;
-    }
     if (g.splitk_ws && (g.M <= 128 || !fused_ln) && g.K % 64 == 0 && g_gemm_variant != 0) {
         // decode step and small prefill (gemm_dec_kernel; M > 128 as 128-row chunks, gridDim.y): the
         // split count depends on N and K only (dec_splits_for), so a row's sums, and the bits of every
