@@ -328,8 +328,12 @@ static bool pick_direct(Context* c, int n_jobs) {
     return n_jobs > 32;
 }
 
-// encoder windows per launch group (32 / 64 / 128 measured the same: 3149-3158 audio-s/s)
-static const int kEncBatch = 32;
+// encoder windows per launch group (round 2: 32 / 64 / 128 measured the same, 3149-3158 audio-s/s);
+// WHISPER_MI355X_ENC_BATCH overrides it (round-6 A/B of the GEMM tile-round quantization)
+static int enc_batch() {
+    static const int v = getenv("WHISPER_MI355X_ENC_BATCH") ? std::max(1, atoi(getenv("WHISPER_MI355X_ENC_BATCH"))) : 32;
+    return v;
+}
 
 // Cross K/V cache for at least `slots` slots (cache form: the call's clips; direct form: the clips
 // whose prompts are too long for the direct prefill). Sized by the calls that use it, so a state
@@ -352,13 +356,13 @@ static void ensure_cross(Context* c, whisper_state* s, int slots) {
 }
 
 // (Re)allocate the workspace for n_jobs clips. Encoder activations are sized for at most
-// kEncBatch windows at once; caches for n_jobs slots. If an allocation fails (out of memory),
+// enc_batch() windows at once; caches for n_jobs slots. If an allocation fails (out of memory),
 // the whole workspace is released and the error propagates: the state stays usable (empty).
 static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
     Workspace& w = s->ws;
     const Hparams& hp = c->hp;
     const size_t d = hp.n_audio_state, nm = hp.n_mels, T = hp.n_audio_ctx, E = esize(c->dt);
-    const int n_enc = std::min(n_jobs, kEncBatch);
+    const int n_enc = std::min(n_jobs, enc_batch());
     if (n_enc > w.cap_enc || n_jobs > w.cap_jobs) drop_graphs(s);
     if (n_enc > w.cap_enc) {
         dfree(w.mel_img); dfree(w.h1); dfree(w.hn); dfree(w.qkv); dfree(w.att); dfree(w.ff); dfree(w.x);
