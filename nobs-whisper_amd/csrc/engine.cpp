@@ -328,10 +328,13 @@ static bool pick_direct(Context* c, int n_jobs) {
     return n_jobs > 32;
 }
 
-// encoder windows per launch group (round 2: 32 / 64 / 128 measured the same, 3149-3158 audio-s/s);
-// WHISPER_MI355X_ENC_BATCH overrides it (round-6 A/B of the GEMM tile-round quantization)
+// encoder windows per launch group. Round 6: 128 (a whole headline batch per launch): the encoder GEMMs'
+// 256 x 256 tiles then fill their last round of 256 CUs (32 windows: QKV 2820 tiles = 11.02 rounds, i.e. a 12th
+// round of 4 tiles; 128 windows: 11250 = 43.9), and the encoder attention's grid is 30 whole rounds: encode
+// 313.6 -> 304.1 ms per step, 3384 -> 3402 audio-s/s (profiles/r06_encb_ab_*.json; round 2 had measured 32 / 64 /
+// 128 the same). ~6.5 GB of encoder activations for large-v3. WHISPER_MI355X_ENC_BATCH overrides it.
 static int enc_batch() {
-    static const int v = getenv("WHISPER_MI355X_ENC_BATCH") ? std::max(1, atoi(getenv("WHISPER_MI355X_ENC_BATCH"))) : 32;
+    static const int v = getenv("WHISPER_MI355X_ENC_BATCH") ? std::max(1, atoi(getenv("WHISPER_MI355X_ENC_BATCH"))) : 128;
     return v;
 }
 
