@@ -755,19 +755,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // the barrier counts of both groups match
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(2);
-    // the next tile's K-tile 0 into buffer 0 (every wave has left both buffers: the barrier above)
     staged0 = false;
-    if constexpr (PRE) {
-        const int nw = wgid + (int)gridDim.x;
-        if (nw < n_tiles) {
-            tile_of(nw, m0, n0);
-            set_src();
-            stage_a(0);
-            stage_b(0);
-            staged0 = true;
-            tile_of(wgid, m0, n0);  // (the epilogue's tile)
-        }
-    }
     constexpr int LDW = 68;  // padded f32 row stride of the staging image
     // staging images in buffer 1, after the part of it the GELU table spills into (PS: buffer 0 holds the next
     // tile's first K-tile)
@@ -824,6 +812,22 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             const float* p = resid_ptr(pq);
 #pragma unroll
             for (int k = 0; k < 4; k++) rx[pq][k] = p ? *(const float4*)(p + 16 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    // PS: the next tile's K-tile 0 into buffer 0 (every wave has left both buffers: the barrier after the main
+    // loop), issued after the bias and the first residual loads so that waiting for those is not behind it
+    // (vmcnt counts in issue order)
+    if constexpr (PRE) {
+        const int nw = wgid + (int)gridDim.x;
+        if (nw < n_tiles) {
+            const int cm0 = m0, cn0 = n0;
+            tile_of(nw, m0, n0);
+            set_src();
+            stage_a(0);
+            stage_b(0);
+            staged0 = true;
+            m0 = cm0;
+            n0 = cn0;
         }
     }
 #pragma unroll
