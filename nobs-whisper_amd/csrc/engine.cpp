@@ -427,7 +427,6 @@ static void ensure_ws_impl(Context* c, whisper_state* s, int n_jobs) {
         dalloc(w.ctl, (size_t)n_jobs * sizeof(SeqCtl));
         dalloc(w.tout, (size_t)n_jobs * sizeof(TokOut));
         dalloc(w.lrec, logits_rec_bytes(n_jobs));
-        WM_CHECK(hipMemset(w.lrec, 0, logits_rec_bytes(n_jobs)));  // the split form's arrival counters start at 0
         dalloc(w.mel_ptrs, (size_t)n_jobs * (2 * sizeof(void*) + 3 * sizeof(int)));
         w.pcm_ptrs = (const float**)(w.mel_ptrs + n_jobs);
         w.n_samp = (int*)(w.pcm_ptrs + n_jobs);

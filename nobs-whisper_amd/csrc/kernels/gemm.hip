@@ -599,11 +599,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const GemmArgs g, const in
 // after its wait. (Issuing all of K-tile kt+2 in P4(kt), a full K-tile ahead, measured 10 %
 // slower: the burst of 8 LDS-DMA per thread in one phase costs more than the extra distance.)
 
-// PS (round 6): persistent tiles. The grid is at most one workgroup per CU and each workgroup walks the tiles
-// wgid, wgid + grid, ... (the same tiles run together as in the one-tile-per-workgroup grid); except for the GELU
-// table epilogues (LT), the next tile's first K-tile is staged into buffer 0 while this tile's epilogue runs
-// (its staging images live in buffer 1), so a tile no longer starts with a full HBM round trip.
-template <typename T, int EPI, bool PS = false>
+template <typename T, int EPI>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int tiles_n, const int gm) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -612,28 +608,20 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, qx = nwg >> 3, rr = nwg & 7;
-    const int wgid0 = (xcd < rr ? xcd * (qx + 1) : rr * (qx + 1) + (xcd - rr) * qx) + (orig >> 3);
-    const int n_tiles = tiles_n * ((g.M + BM - 1) / BM);
+    const int wgid = (xcd < rr ? xcd * (qx + 1) : rr * (qx + 1) + (xcd - rr) * qx) + (orig >> 3);
     // grouped tile order (gm > 0): each group of gm m-tiles walks its m-tiles fastest, so the
     // workgroups an XCD runs at once share B (weight) tiles and a few A tiles in its L2
-    auto tile_of = [&](int wgid, int& m0, int& n0) {
-        int mt = wgid / tiles_n, nt = wgid % tiles_n;
-        if (gm > 0) {
-            const int tiles_m = (g.M + BM - 1) / BM, per = gm * tiles_n, grp = wgid / per, f0 = grp * gm;
-            const int gsz = min(gm, tiles_m - f0), r = wgid - grp * per;
-            mt = f0 + r % gsz;
-            nt = r / gsz;
-        }
-        m0 = mt * BM;
-        n0 = nt * 256;
-    };
-    int m0, n0;
-    tile_of(wgid0, m0, n0);
+    int mt = wgid / tiles_n, nt = wgid % tiles_n;
+    if (gm > 0) {
+        const int tiles_m = (g.M + BM - 1) / BM, per = gm * tiles_n, grp = wgid / per, f0 = grp * gm;
+        const int gsz = min(gm, tiles_m - f0), r = wgid - grp * per;
+        mt = f0 + r % gsz;
+        nt = r / gsz;
+    }
+    const int m0 = mt * BM, n0 = nt * 256;
     // debug stamps (g.stamps): entry, main loop start, main loop end, epilogue end (shader clock), per workgroup
-    // (first tile only)
-    bool first = true;
     auto stamp = [&](int k) {
-        if (g.stamps && first && tid == 0) g.stamps[(long)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memtime();
+        if (g.stamps && tid == 0) g.stamps[(long)blockIdx.x * 4 + k] = __builtin_amdgcn_s_memtime();
     };
     stamp(0);
     const T* A = (const T*)g.A;
@@ -641,20 +629,17 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     // DMA sources: half-tile h (rows h*128 .. +127) = 2 pieces of 8 rows x 128 B per wave
     const T* a_src[2][2];
     const T* b_src[2][2];
-    auto set_src = [&]() {
 #pragma unroll
-        for (int h = 0; h < 2; h++)
+    for (int h = 0; h < 2; h++)
 #pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const int r = h * 128 + (wave * 2 + i) * 8 + (lane >> 3);
-                const int c = (lane & 7) ^ ((r >> 1) & 7);
-                const int m = min(m0 + r, g.M - 1);
-                a_src[h][i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 8;
-                const int n = min(n0 + r, g.N - 1);
-                b_src[h][i] = B + (long)n * g.K + c * 8;
-            }
-    };
-    set_src();
+        for (int i = 0; i < 2; i++) {
+            const int r = h * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((r >> 1) & 7);
+            const int m = min(m0 + r, g.M - 1);
+            a_src[h][i] = A + (m / g.a_rpb) * g.a_bstride + (m % g.a_rpb) * g.a_rstride + c * 8;
+            const int n = min(n0 + r, g.N - 1);
+            b_src[h][i] = B + (long)n * g.K + c * 8;
+        }
     auto stage_a = [&](int kt) {
         u32x4* st = &lds[kt & 1][0];
 #pragma unroll
@@ -674,6 +659,10 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
                                                  (lds_ptr_t)&st[(h * 16 + wave * 2 + i) * 64], 16, 0, 0);
     };
     f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     FT a0[4][2], a1[4][2], b0[2][2], b1[2][2];  // [frag][k-step]
     auto read_a = [&](int buf, int mq, FT (&af)[4][2]) {
 #pragma unroll
@@ -706,24 +695,9 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         asm volatile("s_barrier" ::: "memory");
     };
     const int nk = g.K / BK;
-    constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
-    constexpr bool PRE = PS && !LT;  // the next tile's K-tile 0 staged under the epilogue
-    bool staged0 = false;            // this tile's K-tile 0 already issued (by the previous tile's epilogue)
-    for (int wgid = wgid0; wgid < n_tiles; wgid += PS ? gridDim.x : n_tiles) {
-    if (wgid != wgid0) {
-        tile_of(wgid, m0, n0);
-        set_src();
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // prologue: K-tile 0 (A, B), then B of K-tile 1 and A of K-tile 1
-    if (!staged0) {
-        stage_a(0);
-        stage_b(0);
-    }
-    if (PRE && staged0) __syncthreads();  // every wave is done with the epilogue's staging images (buffer 1)
+    stage_a(0);
+    stage_b(0);
     if (nk > 1) { stage_b(1); stage_a(1); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
@@ -755,15 +729,11 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // the barrier counts of both groups match
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     stamp(2);
-    staged0 = false;
     constexpr int LDW = 68;  // padded f32 row stride of the staging image
-    // staging images in buffer 1, after the part of it the GELU table spills into (PS: buffer 0 holds the next
-    // tile's first K-tile)
-    constexpr int STG_OFF = 12288;
-    float* stg = (float*)((char*)&lds[1][0] + STG_OFF) + wave * 16 * LDW;
-    char* ltab_g = (char*)&lds[0][0];
-    static_assert(kGeluLdsEntries * 2 <= (BM + 256) * 8 * 16 + STG_OFF, "GELU table below the staging images");
-    static_assert(STG_OFF + 8 * 16 * LDW * 4 <= (BM + 256) * 8 * 16, "staging images fit buffer 1");
+    float* stg = (float*)&lds[0][0] + wave * 16 * LDW;
+    constexpr bool LT = EPI == EPI_GELU || EPI == EPI_GELU_POS;
+    char* ltab_g = (char*)&lds[0][0] + 8 * 16 * LDW * 4;  // after the 8 staging images (34816 B)
+    static_assert(8 * 16 * LDW * 4 + kGeluLdsEntries * 2 <= (BM + 256) * 8 * 16 * 2, "GELU table fits");
     if constexpr (LT) {
         gelu_ltab_stage(ltab_g, tid);
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -812,22 +782,6 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             const float* p = resid_ptr(pq);
 #pragma unroll
             for (int k = 0; k < 4; k++) rx[pq][k] = p ? *(const float4*)(p + 16 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    }
-    // PS: the next tile's K-tile 0 into buffer 0 (every wave has left both buffers: the barrier after the main
-    // loop), issued after the bias and the first residual loads so that waiting for those is not behind it
-    // (vmcnt counts in issue order)
-    if constexpr (PRE) {
-        const int nw = wgid + (int)gridDim.x;
-        if (nw < n_tiles) {
-            const int cm0 = m0, cn0 = n0;
-            tile_of(nw, m0, n0);
-            set_src();
-            stage_a(0);
-            stage_b(0);
-            staged0 = true;
-            m0 = cm0;
-            n0 = cn0;
         }
     }
 #pragma unroll
@@ -937,16 +891,11 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         for (int k = 0; k < 16; k++)
             if (colk(k) < g.N) epilogue<EPI, T, true>(g, m, colk(k), v[k]);
     }
-    if (g.stamps && first) {
+    if (g.stamps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         stamp(3);
     }
-    first = false;
-    if constexpr (LT) {
-        if (PS) __syncthreads();  // the GELU table (buffer 0) is read before the next tile's DMA overwrites it
-    }
-    }  // tiles
 }
 
 // fp8 variant of gemm8p_kernel (large-v3-turbo's fp8 weights, BASELINE configs[4]): A and B are
@@ -1843,10 +1792,7 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         else {
             GemmArgs ga = g;
             ga.stamps = g_gemm_stamps;
-            static const int ps = getenv("WHISPER_MI355X_GEMM_PS") ? atoi(getenv("WHISPER_MI355X_GEMM_PS")) : 0;
-            const int tiles = tn * cdiv(g.M, 256);
-            if ((ps || g_gemm_variant == 15) && tiles > 256) gemm8p_kernel<T, EPI, true><<<256, 512, 0, st>>>(ga, tn, gemm_group_m(tn));
-            else gemm8p_kernel<T, EPI><<<tiles, 512, 0, st>>>(ga, tn, gemm_group_m(tn));
+            gemm8p_kernel<T, EPI><<<tn * cdiv(g.M, 256), 512, 0, st>>>(ga, tn, gemm_group_m(tn));
         }
         return;
     }

@@ -253,10 +253,7 @@ struct LogitRec {
     int ix_all, ix_ts, pad;
 };
 
-// Layout: kLogitsCnt arrival counters (one per row of the split form; round 6: the last of a row's KS workgroups
-// combines; zeroed once at allocation, counted modulo KS so they never need a reset), then the records.
-static constexpr int kLogitsCnt = 16;  // = kLogitsSplitMax
-size_t logits_rec_bytes(int n_seq) { return kLogitsCnt * sizeof(unsigned) + (size_t)std::max(1, n_seq) * KS * sizeof(LogitRec); }
+size_t logits_rec_bytes(int n_seq) { return (size_t)std::max(1, n_seq) * KS * sizeof(LogitRec); }
 
 __device__ __forceinline__ void argmax_pair(float& v, int& ix, float ov, int oi) {
     if (ov > v || (ov == v && oi < ix)) { v = ov; ix = oi; }
@@ -292,14 +289,9 @@ __device__ void blk_argmax(float& v, int& ix, float* shv, int* shi) {
     for (int i = 1; i < NW; i++) argmax_pair(v, ix, shv[i], shi[i]);
 }
 
-__device__ __forceinline__ void combine_row(int s, const float* __restrict__ logits, long ld, const SeqCtl* __restrict__ ctl,
-                                            const VocabIds& v, const LogitRec* __restrict__ rec, TokOut* __restrict__ out,
-                                            float* __restrict__ probs, float* sh_lse, int* sh_mask);
-__device__ __forceinline__ void store_rec(LogitRec* p, const LogitRec& r);
 __global__ void __launch_bounds__(LT2) logits_part_kernel(const float* __restrict__ logits, long ld,
                                                           const SeqCtl* __restrict__ ctl, VocabIds v,
-                                                          LogitRec* __restrict__ rec, TokOut* __restrict__ out,
-                                                          float* __restrict__ probs, int fused) {
+                                                          LogitRec* __restrict__ rec) {
     constexpr int NW = LT2 / 64, PER = 14;  // 14 * 256 * 16 >= 51866
     const int c = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, n = v.n_vocab;
     const SeqCtl q = ctl[s];
@@ -355,73 +347,20 @@ __global__ void __launch_bounds__(LT2) logits_part_kernel(const float* __restric
     r.m = m; r.m_ts = mts; r.m_text = mtx; r.ix_all = ix; r.ix_ts = its;
     r.s = blk_sum<NW>(sm, shf);
     r.s_ts = blk_sum<NW>(sts, shf);
-    // the row's last-arriving workgroup combines the KS records (round 6; one launch instead of two): the record
-    // is stored write-through (sc1) and drained before the agent-scope arrival add, the last arriver (its add
-    // returned KS - 1 modulo KS) reads the records with sc1 loads (MI355X_MICROARCH.md, valid forms, row 1)
-    __shared__ int sh_last;
-    __shared__ float sh_lse;
-    __shared__ int sh_mask;
-    if (!fused) {  // (A/B: the separate combine launch)
-        if (tid == 0) rec[(long)s * KS + c] = r;
-        return;
-    }
-    if (tid == 0) {
-        store_rec(rec + (long)s * KS + c, r);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned* cnt = (unsigned*)rec - kLogitsCnt + s;
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh_last = (old % KS) == KS - 1;
-    }
-    __syncthreads();
-    if (sh_last) combine_row(s, logits, ld, ctl, v, rec, out, probs, &sh_lse, &sh_mask);
+    if (tid == 0) rec[(long)s * KS + c] = r;
 }
 
 __global__ void __launch_bounds__(LT2) logits_combine_kernel(const float* __restrict__ logits, long ld,
                                                              const SeqCtl* __restrict__ ctl, VocabIds v,
                                                              const LogitRec* __restrict__ rec, TokOut* __restrict__ out,
                                                              float* __restrict__ probs) {
-    __shared__ float sh_lse;
-    __shared__ int sh_mask;
-    combine_row(blockIdx.x, logits, ld, ctl, v, rec, out, probs, &sh_lse, &sh_mask);
-}
-
-// Pass 2 of row s (every thread of the workgroup calls it). REC: the row's KS records, read by thread 0 with
-// sc1 loads (they come from the other workgroups of this launch, stored write-through: load_rec).
-__device__ __forceinline__ LogitRec load_rec(const LogitRec* p) {
-    const uint64_t* u = (const uint64_t*)p;  // (records are 8-byte aligned: 40 bytes each after a 64-byte header)
-    unsigned w[10];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const uint64_t x = __hip_atomic_load(u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        w[2 * k] = (unsigned)x;
-        w[2 * k + 1] = (unsigned)(x >> 32);
-    }
-    LogitRec r;
-    r.m_r = __builtin_bit_cast(float, w[0]); r.s_r = __builtin_bit_cast(float, w[1]); r.m = __builtin_bit_cast(float, w[2]);
-    r.s = __builtin_bit_cast(float, w[3]); r.m_ts = __builtin_bit_cast(float, w[4]); r.s_ts = __builtin_bit_cast(float, w[5]);
-    r.m_text = __builtin_bit_cast(float, w[6]); r.ix_all = (int)w[7]; r.ix_ts = (int)w[8]; r.pad = (int)w[9];
-    return r;
-}
-__device__ __forceinline__ void store_rec(LogitRec* p, const LogitRec& r) {
-    unsigned* u = (unsigned*)p;
-    const unsigned w[10] = {__builtin_bit_cast(unsigned, r.m_r), __builtin_bit_cast(unsigned, r.s_r), __builtin_bit_cast(unsigned, r.m),
-                            __builtin_bit_cast(unsigned, r.s), __builtin_bit_cast(unsigned, r.m_ts), __builtin_bit_cast(unsigned, r.s_ts),
-                            __builtin_bit_cast(unsigned, r.m_text), (unsigned)r.ix_all, (unsigned)r.ix_ts, (unsigned)r.pad};
-    uint64_t* u8 = (uint64_t*)u;
-#pragma unroll
-    for (int k = 0; k < 5; k++)
-        __hip_atomic_store(u8 + k, (uint64_t)w[2 * k] | ((uint64_t)w[2 * k + 1] << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void combine_row(int s, const float* __restrict__ logits, long ld, const SeqCtl* __restrict__ ctl,
-                                            const VocabIds& v, const LogitRec* __restrict__ rec, TokOut* __restrict__ out,
-                                            float* __restrict__ probs, float* sh_lse, int* sh_mask) {
-    const int tid = threadIdx.x, n = v.n_vocab;
+    const int s = blockIdx.x, tid = threadIdx.x, n = v.n_vocab;
     const SeqCtl q = ctl[s];
     const float* L = logits + (long)s * ld;
+    __shared__ float sh_lse;
+    __shared__ int sh_mask;
     if (tid == 0) {
-        LogitRec R[KS];
-#pragma unroll
-        for (int c = 0; c < KS; c++) R[c] = load_rec(rec + (long)s * KS + c);
+        const LogitRec* R = rec + (long)s * KS;
         float M = -INFINITY, Mts = -INFINITY, Mtx = -INFINITY, Mr = -INFINITY;
         int ix = 0x7fffffff, its = 0x7fffffff;
         for (int c = 0; c < KS; c++) {
@@ -460,13 +399,13 @@ __device__ __forceinline__ void combine_row(int s, const float* __restrict__ log
         r.nosp_prob = q.want_nosp ? expf(L[v.nosp] - (logf(Sr) + Mr)) : 0.0f;
         r.pad = 0.0f;
         out[s] = r;
-        *sh_lse = lse;
-        *sh_mask = mask_text;
+        sh_lse = lse;
+        sh_mask = mask_text;
     }
     if (!q.want_probs) return;
     __syncthreads();
-    const float lse = *sh_lse;
-    const bool mask_text = *sh_mask;
+    const float lse = sh_lse;
+    const bool mask_text = sh_mask;
     for (int i = tid; i < n; i += LT2) {
         float xv = masked_logit(L[i], i, q, v);
         if (mask_text && i < v.beg) xv = -INFINITY;
@@ -477,19 +416,14 @@ __device__ __forceinline__ void combine_row(int s, const float* __restrict__ log
 
 // rows up to this count take the split form (16 chunk workgroups per row + a combine)
 static const int kLogitsSplitMax = 16;
-static_assert(kLogitsSplitMax <= kLogitsCnt, "an arrival counter per row of the split form");
 
 void launch_logits(const float* logits, long ld, const SeqCtl* ctl, int n_seq, const VocabIds& v, TokOut* out, float* probs,
                    void* rec, hipStream_t st) {
     if (n_seq <= 0) return;
     if (v.n_vocab > NPT * LT) WM_FAIL("vocabulary %d > %d", v.n_vocab, NPT * LT);
     if (rec && n_seq <= kLogitsSplitMax && v.n_vocab <= 14 * LT2 * KS) {
-        // (records after the counters; kLogitsCnt >= kLogitsSplitMax rows). WHISPER_MI355X_LOGITS_FUSED=0: the round-5
-        // form, a second launch combines (A/B)
-        static const int fused = getenv("WHISPER_MI355X_LOGITS_FUSED") ? atoi(getenv("WHISPER_MI355X_LOGITS_FUSED")) : 1;
-        LogitRec* R = (LogitRec*)((char*)rec + kLogitsCnt * sizeof(unsigned));
-        logits_part_kernel<<<dim3(KS, n_seq), LT2, 0, st>>>(logits, ld, ctl, v, R, out, probs, fused);
-        if (!fused) logits_combine_kernel<<<n_seq, LT2, 0, st>>>(logits, ld, ctl, v, R, out, probs);
+        logits_part_kernel<<<dim3(KS, n_seq), LT2, 0, st>>>(logits, ld, ctl, v, (LogitRec*)rec);
+        logits_combine_kernel<<<n_seq, LT2, 0, st>>>(logits, ld, ctl, v, (const LogitRec*)rec, out, probs);
         return;
     }
     logits_kernel<<<n_seq, LT, (size_t)NPT_LDS * LT * sizeof(float), st>>>(logits, ld, ctl, v, out, probs);
