@@ -1108,29 +1108,35 @@ __global__ void __launch_bounds__(256) quant_rows_fp8_kernel(const T* __restrict
 // (row>>2)&3), each lane's 8 bytes are widened to the MFMA type in registers (exact: e4m3 values are
 // representable in f16 and bf16) and the column scale multiplies the f32 sum before the store. Half
 // the weight bytes of the decode step; the activations stay in the compute type.
-template <typename T, int EPI, bool SPLIT, int AUXB = 0, bool W8 = false>
+// BM (round 6): rows per workgroup, 128, 64 or 32. Steps of <= 32 clips (the 8-GPU shard of configs[3]: 16 per
+// rank) staged 128 A rows per K-tile of which 96+ repeated the last row (clamped); BM = 32 / 64 stage only about
+// the rows that exist (M = 16: 8.2 -> 7.1 us per xq GEMM, the 16-clip line 1106 -> 1172 audio-s/s). Every output's k order (K-tiles, then the two 32-deep MFMA steps) is the same for both, so the bits are.
+template <typename T, int EPI, bool SPLIT, int AUXB = 0, bool W8 = false, int BM = 128>
 __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const int kc) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    constexpr int BM = 128, BN = 64, BK = 64, MAXT = 4;
+    constexpr int BN = 64, BK = 64, MAXT = 4;
+    constexpr int MI = BM / 32;  // row fragments per wave (2 x 2 waves, BM / 2 rows each)
+    constexpr int AP = BM / 32;  // A pieces (8 rows x 128 B) per wave and stage
+    static_assert(BM == 128 || BM == 64 || BM == 32, "BM");
     constexpr int BCH = W8 ? 4 : 8;             // 16-byte chunks per B row
     constexpr int STAGE = BM * 8 + BN * BCH;    // u32x4 per stage
     __shared__ u32x4 lds[MAXT * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each 64 rows x 32 columns
+    const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each BM / 2 rows x 32 columns
     const int n0 = blockIdx.x * BN;
     const int m0 = blockIdx.y * BM;  // row chunk (prefill: M > 128 as chunks of 128 rows, same math per row)
     const int k0 = SPLIT ? blockIdx.z * kc : 0;
     const int nkt = min(kc, g.K - k0) / BK;
     const T* A = (const T*)g.A;
     const T* B = (const T*)g.B;
-    // per stage: A = 16 pieces of 8 rows (4 per wave), B = 8 pieces (2 per wave)
-    const T* a_src[4];
+    // per stage: A = BM / 8 pieces of 8 rows (AP per wave), B = 8 pieces (2 per wave)
+    const T* a_src[AP];
     const T* b_src[2];
     const uint8_t* b8_src = nullptr;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+    for (int i = 0; i < AP; i++) {
+        const int r = (wave * AP + i) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         const int m = min(m0 + r, g.M - 1);
         a_src[i] = A + (long)m * g.a_rstride + k0 + c * 8;
@@ -1152,8 +1158,8 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
     auto issue = [&](int t) {
         u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&st[(wave * 4 + i) * 64], 16, 0, 0);
+        for (int i = 0; i < AP; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + t * BK), (lds_ptr_t)&st[(wave * AP + i) * 64], 16, 0, 0);
         if constexpr (W8) {
             __builtin_amdgcn_global_load_lds((const void*)(b8_src + t * BK), (lds_ptr_t)&st[BM * 8 + wave * 64], 16, 0, AUXB);
         } else {
@@ -1162,11 +1168,11 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
                 __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + t * BK), (lds_ptr_t)&st[BM * 8 + (wave * 2 + i) * 64], 16, 0, AUXB);
         }
     };
-    constexpr int PER_STAGE = W8 ? 5 : 6;  // DMA instructions per wave and stage
+    constexpr int PER_STAGE = AP + (W8 ? 1 : 2);  // DMA instructions per wave and stage
     for (int t = 0; t < min(nkt, MAXT); t++) issue(t);
-    f32x4 acc[4][2];
+    f32x4 acc[MI][2];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < MI; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < nkt; t++) {
@@ -1177,7 +1183,23 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
             else if (ahead == 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
             else if (ahead == 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if constexpr (PER_STAGE == 4) {
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if constexpr (PER_STAGE == 3) {
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if constexpr (PER_STAGE == 2) {
+            if (ahead >= 3) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         } else {
+            static_assert(PER_STAGE == 5, "vmcnt table");
             if (ahead >= 3) asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
             else if (ahead == 2) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
             else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
@@ -1186,11 +1208,11 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         const u32x4* st = &lds[(t & (MAXT - 1)) * STAGE];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            FT af[4], bfr[2];
+            FT af[MI], bfr[2];
             const int ch = s * 4 + (lane >> 4);
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int row = wm * 64 + i * 16 + (lane & 15);
+            for (int i = 0; i < MI; i++) {
+                const int row = wm * (BM / 2) + i * 16 + (lane & 15);
                 af[i] = __builtin_bit_cast(FT, st[row * 8 + (ch ^ ((row >> 1) & 7))]);
             }
 #pragma unroll
@@ -1220,7 +1242,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 4; i++)
+            for (int i = 0; i < MI; i++)
 #pragma unroll
                 for (int j = 0; j < 2; j++) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
         }
@@ -1230,7 +1252,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < MI; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             const int n = n0 + wn * 32 + j * 16 + (lane & 15);
@@ -1238,7 +1260,7 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
             const float wsc = W8 ? g.w8_scale[n] : 1.0f;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
                 if (m >= g.M) continue;
                 const float v = W8 ? acc[i][j][r] * wsc : acc[i][j][r];
                 if constexpr (SPLIT) {
@@ -1257,6 +1279,27 @@ __global__ void __launch_bounds__(256) gemm_dec_kernel(const GemmArgs g, const i
 // pipelined, 4 256^2 phase-interleaved (the auto choice for big GEMMs)
 int g_gemm_variant = -1;
 unsigned long long* g_gemm_stamps = nullptr;
+
+// gemm_dec_kernel row tile: the smallest of 32 / 64 / 128 rows that holds the step (the grid's row chunks
+// stay cdiv(M, 128): a smaller tile is only taken when one tile holds every row). WHISPER_MI355X_DEC_BM caps
+// the tile from below for the A/B (128: always 128 rows, the round-5 kernel).
+static int dec_bm_min() {
+    static const int v = getenv("WHISPER_MI355X_DEC_BM") ? atoi(getenv("WHISPER_MI355X_DEC_BM")) : 32;
+    return v;
+}
+template <typename T, int EPI, bool SPLIT, bool W8>
+static void launch_dec(const GemmArgs& g, int tiles, int splits, int kc, hipStream_t st) {
+    if (g.M <= 32 && dec_bm_min() <= 32) {
+        gemm_dec_kernel<T, EPI, SPLIT, 2, W8, 32><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    } else if (g.M <= 64 && dec_bm_min() <= 64) {
+        gemm_dec_kernel<T, EPI, SPLIT, 2, W8, 64><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    } else {
+        // 65..128 rows stay one 128-row tile: two 64-row chunks (on gridDim.y, or 8 ids apart so both land on one
+        // XCD's L2) read each weight tile twice and measured slower in the 128-clip step (decode 809 -> 832-840 ms,
+        // profiles/r06_bm_m64_ab_*.json) though some isolated shapes gained (xq 11.9 -> 10.7 us)
+        gemm_dec_kernel<T, EPI, SPLIT, 2, W8, 128><<<dim3(tiles, cdiv(g.M, 128), splits), 256, 0, st>>>(g, kc);
+    }
+}
 
 template <typename T, int EPI>
 __global__ void splitk_reduce_kernel(const GemmArgs g, int splits) {
@@ -1815,7 +1858,6 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
         // K-tiles measured faster in isolation, 9.6 vs 10.4 us at N = K = 1280, but not in the decode
         // step: 82.0 vs 81.6 us of GEMM + reduce per layer.)
         const int tiles = cdiv(g.N, 64);
-        const int mch = cdiv(g.M, 128);
         int splits = dec_splits_for(tiles, nk);
         if (dec_splits_override() > 0) splits = std::min(dec_splits_override(), nk);
         // unsplit at M <= 64 (the logits GEMM of a small batch): the 64-row register-staged kernel
@@ -1826,12 +1868,12 @@ static void launch_t(const GemmArgs& g, hipStream_t st) {
             const int kc = cdiv(nk, splits) * 64;
             splits = cdiv(g.K, kc);
             if (splits == 1 && !fused_ln) {
-                if (g.w8_scale) gemm_dec_kernel<T, EPI, false, 2, true><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
-                else gemm_dec_kernel<T, EPI, false, 2><<<dim3(tiles, mch), 256, 0, st>>>(g, kc);
+                if (g.w8_scale) launch_dec<T, EPI, false, true>(g, tiles, 1, kc, st);
+                else launch_dec<T, EPI, false, false>(g, tiles, 1, kc, st);
                 return;
             }
-            if (g.w8_scale) gemm_dec_kernel<T, EPI, true, 2, true><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
-            else gemm_dec_kernel<T, EPI, true, 2><<<dim3(tiles, mch, splits), 256, 0, st>>>(g, kc);
+            if (g.w8_scale) launch_dec<T, EPI, true, true>(g, tiles, splits, kc, st);
+            else launch_dec<T, EPI, true, false>(g, tiles, splits, kc, st);
             if (fused_ln) {
                 launch_reduce_resid_ln<T>(g, splits, st);
             } else {
@@ -1910,8 +1952,8 @@ static int launch_partials_t(const GemmArgs& g, hipStream_t st) {
     const int kc = cdiv(nk, splits) * 64;
     splits = cdiv(g.K, kc);
     if ((long)splits * g.M * g.N > g.splitk_ws_elems) return 0;
-    if (g.w8_scale) gemm_dec_kernel<T, EPI_STORE, true, 2, true><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
-    else gemm_dec_kernel<T, EPI_STORE, true, 2><<<dim3(tiles, 1, splits), 256, 0, st>>>(g, kc);
+    if (g.w8_scale) launch_dec<T, EPI_STORE, true, true>(g, tiles, splits, kc, st);
+    else launch_dec<T, EPI_STORE, true, false>(g, tiles, splits, kc, st);
     return splits;
 }
 
