@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0       # dense bf16/f16 MFMA peak (no sparsity)
 FP8_PEAK_TFS = 5000.0        # dense fp8 MFMA peak
 # PMC traffic pass of the roofline kernel (tools/pmc.sh -> tools/pmc_traffic.py), chosen by name
-PMC_TRAFFIC_FILE = "r05_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r06_pmc_traffic.json"
 KT_LAYER_STRIDE = 8
 
 
