@@ -171,12 +171,24 @@ __global__ void __launch_bounds__(256) attn_enc_kernel(const T* __restrict__ qkv
 // so the compiler cannot re-pack them) instead of v_pk_fma_f32 / v_pk_add_f32, which the guide prices
 // above two scalar ops beside MFMAs; the same per-element operations, so the same bits. No VGPR spill at
 // 128 (variant 5: 2); encode 325.9 -> 324.6 ms per step at 128 clips (profiles/r03_attn_encoder_variants.txt).
+// XCD (round 6): a 1-D grid of nqb x H x B workgroups whose id L runs on XCD L % 8; workgroup L takes the
+// (query block, head, window) of index (L % 8) * (G / 8) + L / 8, so the query blocks of one (window, head)
+// share an XCD and its L2 fetches their K / V once (id order: they were consecutive ids, i.e. up to 6
+// XCDs, each fetching the same 384 KB). Same work per workgroup, same bits.
 template <typename T, int MINW = 1, bool PK = true>
-__global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d) {
+__global__ void __launch_bounds__(512, MINW) attn_enc2_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int d,
+                                                             int nqb = 0, int H = 0) {
     typedef typename Frag<T>::type FT;
     typedef short v4s __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) v4s* lds_v4s_t;
-    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    if (nqb > 0) {
+        const int L = blockIdx.x, G = gridDim.x;
+        const int p = (L & 7) * (G >> 3) + (L >> 3);
+        qb = p % nqb;
+        h = (p / nqb) % H;
+        b = p / (nqb * H);
+    }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int hh = lane >> 5, ql = lane & 31;
     const long base = (long)b * Tn;
@@ -1027,6 +1039,12 @@ void launch_attn_prefill(DType dt, const void* q, int q_stride, const void* cach
                                                           (const int2*)tiles, L, layer, H, ctx, d, (bf16_t*)out);
 }
 
+// XCD-grouped encoder attention grid (attn_enc2_kernel): WHISPER_MI355X_ENC_ATTN_XCD=0 keeps the 3-D grid (A/B)
+static bool attn_enc_xcd() {
+    static const bool v = !getenv("WHISPER_MI355X_ENC_ATTN_XCD") || atoi(getenv("WHISPER_MI355X_ENC_ATTN_XCD")) != 0;
+    return v;
+}
+
 void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, int d, int H, hipStream_t st,
                          int variant_arg) {
     // variant 6 (attn_enc2_kernel, 128 VGPRs, scalar softmax FMAs) unless a kernel benchmark asks for
@@ -1039,7 +1057,14 @@ void launch_attn_encoder(DType dt, const void* qkv, void* out, int B, int Tn, in
         return;
     }
     if (variant == 6 && d == H * 64) {
-        dim3 grid(cdiv(Tn, 256), H, B);
+        const int nqb = cdiv(Tn, 256);
+        if ((long)nqb * H * B % 8 == 0 && attn_enc_xcd()) {
+            const int G = nqb * H * B;
+            if (dt == DType::F16) attn_enc2_kernel<half_t, 4, false><<<G, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d, nqb, H);
+            else attn_enc2_kernel<bf16_t, 4, false><<<G, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d, nqb, H);
+            return;
+        }
+        dim3 grid(nqb, H, B);
         if (dt == DType::F16) attn_enc2_kernel<half_t, 4, false><<<grid, 512, 0, st>>>((const half_t*)qkv, (half_t*)out, Tn, d);
         else attn_enc2_kernel<bf16_t, 4, false><<<grid, 512, 0, st>>>((const bf16_t*)qkv, (bf16_t*)out, Tn, d);
         return;
