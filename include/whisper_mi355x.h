@@ -146,6 +146,9 @@ WHISPER_API int whisper_mi355x_debug_gemm_small(struct whisper_context * ctx, in
                                                 const void * B, int N, const float * bias, void * out,
                                                 const float * ln_w, const float * ln_b, int reps, float * ms);
 WHISPER_API void whisper_mi355x_set_dec_splits(int splits); /* 0 = heuristic */
+/* Test hook: the split-K decode GEMM's smallest row tile (32, 64 or 128; 0 = WHISPER_MI355X_DEC_BM or 32).
+ * A step takes the smallest tile holding its rows; every value gives the same bits. */
+WHISPER_API void whisper_mi355x_set_dec_bm(int rows);
 /* Test hook: a persistent decode step's waits give up after this many 100 MHz ticks (default 5,000,000 =
  * 50 ms); 0 makes every persistent launch give up, so each step takes the re-run path. Decode graphs
  * captured before the call are retired (not replayed) once it changes the value; likewise for the stamps

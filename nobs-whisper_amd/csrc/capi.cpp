@@ -10,7 +10,7 @@
 #include "../../include/whisper_mi355x.h"
 #include "engine.h"
 
-namespace wm { extern int g_gemm_variant; extern int g_dec_splits; extern unsigned long long* g_gemm_stamps; }
+namespace wm { extern int g_gemm_variant; extern int g_dec_splits; extern int g_dec_bm; extern unsigned long long* g_gemm_stamps; }
 using namespace wm;
 
 static Context* C(whisper_context* ctx) { return ctx ? &ctx->c : nullptr; }
@@ -563,6 +563,7 @@ int whisper_mi355x_kernel_stats(struct whisper_state* s, int cls, double out[3])
 void whisper_mi355x_set_gemm_variant(int v) { wm::g_gemm_variant = v; }
 void whisper_mi355x_set_gemm_stamps(void* dev) { wm::g_gemm_stamps = (unsigned long long*)dev; }
 void whisper_mi355x_set_dec_splits(int splits) { wm::g_dec_splits = splits; }
+void whisper_mi355x_set_dec_bm(int rows) { wm::g_dec_bm = rows; }
 void whisper_mi355x_set_pdec_spin(long ticks) {
     wm::g_pdec_spin_ticks = ticks;
     wm::g_pdec_gen.fetch_add(1, std::memory_order_release);

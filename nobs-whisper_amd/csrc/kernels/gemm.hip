@@ -1281,11 +1281,13 @@ int g_gemm_variant = -1;
 unsigned long long* g_gemm_stamps = nullptr;
 
 // gemm_dec_kernel row tile: the smallest of 32 / 64 / 128 rows that holds the step (the grid's row chunks
-// stay cdiv(M, 128): a smaller tile is only taken when one tile holds every row). WHISPER_MI355X_DEC_BM caps
-// the tile from below for the A/B (128: always 128 rows, the round-5 kernel).
+// stay cdiv(M, 128): a smaller tile is only taken when one tile holds every row). WHISPER_MI355X_DEC_BM (or
+// whisper_mi355x_set_dec_bm, a test hook) caps the tile from below for the A/B (128: always 128 rows, the
+// round-5 kernel). Every value gives the same bits.
+int g_dec_bm = 0;  // 0: the environment's value (default 32)
 static int dec_bm_min() {
     static const int v = getenv("WHISPER_MI355X_DEC_BM") ? atoi(getenv("WHISPER_MI355X_DEC_BM")) : 32;
-    return v;
+    return g_dec_bm > 0 ? g_dec_bm : v;
 }
 template <typename T, int EPI, bool SPLIT, bool W8>
 static void launch_dec(const GemmArgs& g, int tiles, int splits, int kc, hipStream_t st) {

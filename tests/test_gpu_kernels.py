@@ -282,3 +282,31 @@ def test_attn_encoder_variant_timing(wrs, micro_model):
     L.whisper_mi355x_dev_free(c.ptr, C.c_void_p(p))
     c.close()
     print("attn_encoder 32 x 1500 x 20 heads: " + ", ".join(line))
+
+
+@pytest.mark.parametrize("M", [1, 16, 32, 33, 64, 100])
+def test_dec_gemm_row_tiles_bitwise(wrs, micro_model, M):
+    """The split-K decode GEMM's row tile (32 / 64 / 128 rows, gemm.hip launch_dec) changes no output bit:
+    every output keeps its k order. Large-v3 decode shapes, f16 and bf16, store / GELU / f32 epilogues; the
+    128-row tile (whisper_mi355x_set_dec_bm(128)) against the default (the smallest tile holding M rows)."""
+    L = wrs.lib()
+    L.whisper_mi355x_set_dec_bm.argtypes = [C.c_int]
+    for dt in (wrs.F16, wrs.BF16):
+        c = wrs.WhisperContext(micro_model, dtype=dt)
+        try:
+            for (N, K, epi) in [(3840, 1280, 4), (1280, 1280, 0), (5120, 1280, 1), (1280, 5120, 4)]:
+                rng = np.random.default_rng(M * 31 + N + K)
+                A = rng.standard_normal((M, K)).astype(np.float16)
+                B = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+                bias = (0.1 * rng.standard_normal(N)).astype(np.float32)
+                outs = []
+                for bm in (128, 0):
+                    L.whisper_mi355x_set_dec_bm(bm)
+                    try:
+                        outs.append(_run_gemm(wrs, c, A, B, bias, -1, epi=epi)[0])
+                    finally:
+                        L.whisper_mi355x_set_dec_bm(0)
+                assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8)), (dt, N, K, epi)
+                assert np.isfinite(outs[1].astype(np.float32)).all()
+        finally:
+            c.close()
