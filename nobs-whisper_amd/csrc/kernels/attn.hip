@@ -1133,7 +1133,12 @@ void launch_attn_self_step(DType dt, const DecSlabs& sl, void* cache, const int*
                            int layer, int H, int ctx, int d, void* out, hipStream_t st) {
     if (n <= 0) return;
     if (ctx > 448) WM_FAIL("self-attention context %d > 448", ctx);
-    const int hpb = H % 4 == 0 ? 4 : H % 2 == 0 ? 2 : 1;
+    // heads (waves) per workgroup: 1 up to 32 clips (16 clips: decode 346.4 -> 342.7 ms per step), 4 above (128
+    // clips: the same within noise); profiles/r06_self_hpb_ab.txt. WHISPER_MI355X_SELF_HPB (1 / 2 / 4) forces it for
+    // an A/B. The waves of a workgroup share no data, so every value gives the same bits.
+    static const int hpb_env = getenv("WHISPER_MI355X_SELF_HPB") ? atoi(getenv("WHISPER_MI355X_SELF_HPB")) : 0;
+    const int want = hpb_env > 0 ? hpb_env : (n <= 32 ? 1 : 4);
+    const int hpb = want >= 4 && H % 4 == 0 ? 4 : want >= 2 && H % 2 == 0 ? 2 : 1;
     // default-policy K/V reads (non-temporal measured 3048-3053 vs 3050-3057 audio-s/s, not kept)
 #define WM_SELF(TT, HB) \
     attn_self_step_kernel<TT, HB, false><<<dim3(n, H / HB), 64 * HB, 0, st>>>(sl, (TT*)cache, slot, pos, L, layer, H, ctx, d, (TT*)out)
