@@ -130,7 +130,8 @@ WHISPER_API int whisper_mi355x_kernel_stats(struct whisper_state * state, int cl
 WHISPER_API long whisper_mi355x_pdec_give_ups(struct whisper_state * state);
 
 /* Kernel-level test/tuning hooks (device pointers): one fused-epilogue GEMM launch of the engine
- * (epi as in kernels.h: 0 store, 1 gelu, 2 residual f32, 4 f32), averaged over reps; and the
+ * (epi as in kernels.h: 0 store, 1 gelu, 2 residual f32, 4 f32, 5 cross K/V: out is then a cross cache of
+ * M / n_audio_ctx slots for N / 2K layers, K = d), averaged over reps; and the
  * GEMM variant override (-1 auto, 0 register-staged, 1 LDS-DMA). */
 WHISPER_API int whisper_mi355x_debug_gemm(struct whisper_context * ctx, int epi, const void * A, int M, int K,
                                           const void * B, int N, const float * bias, void * out, int reps, float * ms);

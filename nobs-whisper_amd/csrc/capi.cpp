@@ -601,6 +601,16 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
             g.splitk_ws_elems = 64L * M * N;
             WM_CHECK(hipMalloc(&g.splitk_ws, g.splitk_ws_elems * sizeof(float)));
         }
+        int* dslot = nullptr;
+        if (epi == EPI_CROSSKV) {  // out = a cross cache [M / n_audio_ctx][N / 2K][2][K / 64][n_audio_ctx][64], slots in order
+            const int T = ctx->c.hp.n_audio_ctx;
+            if (M % T != 0 || K % 64 != 0 || N % (2 * K) != 0) return -1;
+            std::vector<int> hs(M / T);
+            for (int i = 0; i < M / T; i++) hs[i] = i;
+            WM_CHECK(hipMalloc((void**)&dslot, hs.size() * sizeof(int)));
+            WM_CHECK(hipMemcpy(dslot, hs.data(), hs.size() * sizeof(int), hipMemcpyHostToDevice));
+            g.cache = out; g.row_slot = dslot; g.d = K; g.H = K / 64; g.ctx = T; g.L = N / (2 * K); g.layer = 0;
+        }
         hipEvent_t e0, e1;
         WM_CHECK(hipEventCreate(&e0));
         WM_CHECK(hipEventCreate(&e1));
@@ -616,6 +626,7 @@ int whisper_mi355x_debug_gemm(struct whisper_context* ctx, int epi, const void* 
         hipEventDestroy(e1);
         hipStreamDestroy(st);
         if (g.splitk_ws) hipFree(g.splitk_ws);
+        if (dslot) hipFree(dslot);
         return 0;
     });
 }

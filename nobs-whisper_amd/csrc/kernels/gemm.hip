@@ -784,6 +784,62 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
             for (int k = 0; k < 4; k++) rx[pq][k] = p ? *(const float4*)(p + 16 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
+    // EPI_CROSSKV (round 6): the wave's 64 columns are one head of one layer's K or V, and a row of its cache plane
+    // [slot][L][2][H][ctx][64] is 128 contiguous bytes. Lane (r8 = lane >> 3, c8 = 8 (lane & 7)) writes 8 columns of
+    // rows r8 and r8 + 8 of a sub-tile, so every store instruction writes 8 whole consecutive rows, 1 KiB
+    // contiguous. (The generic lane map below writes 16 half rows per instruction: the K/V GEMM of a large-v3
+    // layer at 128 clips took 2.84 ms against 1.49 ms for the same shape with a row-major store,
+    // tools/debug/xkv_shape.py.) Same arithmetic: (acc + bias) * scale for K, rounded once.
+    bool xdone = false;
+    if constexpr (EPI == EPI_CROSSKV) {
+        if (full) {
+            const int r8 = lane >> 3, c8 = (lane & 7) * 8, n = nb + c8;
+            float b8[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) b8[k] = g.bias ? g.bias[n + k] : 0.0f;
+            const int l = g.layer + n / (2 * g.d), kv = (n / g.d) & 1, hh = (n % g.d) >> 6, dh = n & 63;
+            const float sc = kv == 0 ? g.scale : 1.0f;
+            const long colpart = (((long)l * 2 + kv) * g.H + hh) * g.ctx * 64 + dh;
+            const long sstride = (long)g.L * 2 * g.H * g.ctx * 64;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) stg[((lane >> 4) * 4 + r) * LDW + j * 16 + (lane & 15)] = acc[i][j][r];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                float x[2][8];
+#pragma unroll
+                for (int h2 = 0; h2 < 2; h2++) {
+                    const float4 a = *(const float4*)(stg + (r8 + 8 * h2) * LDW + c8);
+                    const float4 b = *(const float4*)(stg + (r8 + 8 * h2) * LDW + c8 + 4);
+                    x[h2][0] = a.x; x[h2][1] = a.y; x[h2][2] = a.z; x[h2][3] = a.w;
+                    x[h2][4] = b.x; x[h2][5] = b.y; x[h2][6] = b.z; x[h2][7] = b.w;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int h2 = 0; h2 < 2; h2++) {
+                    const int m = m0 + wm * 128 + i * 16 + r8 + 8 * h2;
+                    if (m >= g.M) continue;
+                    const int bb = m / g.ctx, t = m - bb * g.ctx;
+                    T o[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        float v = x[h2][k];
+                        if (g.bias) v = v + b8[k];
+                        if (sc != 1.0f) v = v * sc;
+                        o[k] = (T)v;
+                    }
+                    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                    *(u4*)((T*)g.cache + (long)g.row_slot[bb] * sstride + colpart + (long)t * 64) = *(const u4*)&o[0];
+                }
+            }
+            xdone = true;
+        }
+    }
+    if (!xdone) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         float4 cur[4];
@@ -891,6 +947,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
         for (int k = 0; k < 16; k++)
             if (colk(k) < g.N) epilogue<EPI, T, true>(g, m, colk(k), v[k]);
     }
+    }  // !xdone
     if (g.stamps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
