@@ -790,17 +790,30 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
     // contiguous. (The generic lane map below writes 16 half rows per instruction: the K/V GEMM of a large-v3
     // layer at 128 clips took 2.84 ms against 1.49 ms for the same shape with a row-major store,
     // tools/debug/xkv_shape.py.) Same arithmetic: (acc + bias) * scale for K, rounded once.
+    // EPI_QKV_DEC (the prefill's QKV projection: q rows to out, k / v rows into the self cache at each row's
+    // position, consecutive positions for a clip's prompt) takes the same map; it went per element before.
     bool xdone = false;
-    if constexpr (EPI == EPI_CROSSKV) {
-        if (full) {
+    if constexpr (EPI == EPI_CROSSKV || EPI == EPI_QKV_DEC) {
+        if (full && (EPI == EPI_CROSSKV || ((((uintptr_t)g.out) & 15) == 0 && (g.ldo & 7) == 0 && g.d % 64 == 0))) {
             const int r8 = lane >> 3, c8 = (lane & 7) * 8, n = nb + c8;
             float b8[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) b8[k] = g.bias ? g.bias[n + k] : 0.0f;
-            const int l = g.layer + n / (2 * g.d), kv = (n / g.d) & 1, hh = (n % g.d) >> 6, dh = n & 63;
-            const float sc = kv == 0 ? g.scale : 1.0f;
-            const long colpart = (((long)l * 2 + kv) * g.H + hh) * g.ctx * 64 + dh;
-            const long sstride = (long)g.L * 2 * g.H * g.ctx * 64;
+            float sc;
+            long colpart, sstride;
+            int part = 0;
+            if constexpr (EPI == EPI_CROSSKV) {
+                const int l = g.layer + n / (2 * g.d), kv = (n / g.d) & 1, hh = (n % g.d) >> 6, dh = n & 63;
+                sc = kv == 0 ? g.scale : 1.0f;
+                colpart = (((long)l * 2 + kv) * g.H + hh) * g.ctx * 64 + dh;
+                sstride = (long)g.L * 2 * g.H * g.ctx * 64;
+            } else {
+                part = n / g.d;  // 0 q, 1 k, 2 v
+                const int nn = n - part * g.d, hh = nn >> 6, dh = nn & 63;
+                sc = part <= 1 ? g.scale : 1.0f;
+                colpart = (((long)g.layer * 2 + (part == 2)) * g.H + hh) * g.ctx * 64 + dh;
+                sstride = (long)g.L * 2 * g.H * g.ctx * 64;
+            }
 #pragma unroll
             for (int i = 0; i < 8; i++) {
 #pragma unroll
@@ -823,17 +836,26 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const GemmArgs g, const int
                 for (int h2 = 0; h2 < 2; h2++) {
                     const int m = m0 + wm * 128 + i * 16 + r8 + 8 * h2;
                     if (m >= g.M) continue;
-                    const int bb = m / g.ctx, t = m - bb * g.ctx;
                     T o[8];
 #pragma unroll
                     for (int k = 0; k < 8; k++) {
                         float v = x[h2][k];
                         if (g.bias) v = v + b8[k];
-                        if (sc != 1.0f) v = v * sc;
+                        if (EPI == EPI_QKV_DEC && part == 0) v = v * sc;  // (q: always scaled, as the element form)
+                        else if (sc != 1.0f) v = v * sc;
                         o[k] = (T)v;
                     }
                     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                    *(u4*)((T*)g.cache + (long)g.row_slot[bb] * sstride + colpart + (long)t * 64) = *(const u4*)&o[0];
+                    T* dst;
+                    if constexpr (EPI == EPI_CROSSKV) {
+                        const int bb = m / g.ctx, t = m - bb * g.ctx;
+                        dst = (T*)g.cache + (long)g.row_slot[bb] * sstride + colpart + (long)t * 64;
+                    } else if (part == 0) {
+                        dst = (T*)g.out + (long)m * g.ldo + n;
+                    } else {
+                        dst = (T*)g.cache + (long)g.row_slot[m] * sstride + colpart + (long)g.row_pos[m] * 64;
+                    }
+                    *(u4*)dst = *(const u4*)&o[0];
                 }
             }
             xdone = true;

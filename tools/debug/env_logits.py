@@ -1,6 +1,6 @@
 """Dump teacher-forced decode logits (spot clips 0 and n-1) of an n-clip batch to gpurun_out/envlg_<tag>.npy, for a
 bitwise A/B of engine switches that must not change any bit (run once per setting: the switches are read once per
-process). Usage: [WHISPER_MI355X_<SWITCH>=v] python tools/debug/env_logits.py <tag> [n] [cache|direct]
+process). Usage: [WHISPER_MI355X_<SWITCH>=v] python tools/debug/env_logits.py <tag> [n] [cache|direct] [prompt]
              python tools/debug/env_logits.py --compare <tagA> <tagB>"""
 import os
 import sys
@@ -26,7 +26,8 @@ ctx = wrs.WhisperContext(model_path("large-v3-2L+conf"), dtype=wrs.BF16)
 st = ctx.create_state()
 V = wrs.lib().whisper_n_vocab(ctx.ptr)
 forced = np.full((n, ntok), 50364, np.int32)
-rc, lg = st.full_batch_forced(wrs.reference_full_params("en"), [synthetic_pcm(k) for k in range(n)], ntok, forced, [0, n - 1], V)
+prm = wrs.reference_full_params("en", wrs.DEFAULT_VOCABULARY if len(sys.argv) > 4 and sys.argv[4] == "prompt" else None)
+rc, lg = st.full_batch_forced(prm, [synthetic_pcm(k) for k in range(n)], ntok, forced, [0, n - 1], V)
 assert rc == 0
 np.save(os.path.join("gpurun_out", f"envlg_{sys.argv[1]}.npy"), lg)
 print(sys.argv[1], n, lg.shape, float(np.abs(lg).max()))
