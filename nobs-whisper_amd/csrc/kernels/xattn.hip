@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) xattn_qproj_kernel(const T* __restrict__ 
 template <typename T, int NW, int CT, int AUX>
 __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict__ enc, const int* __restrict__ slot,
                                                              const T* __restrict__ qx, int Tn, int splits, float thr,
-                                                             float* __restrict__ opart, float* __restrict__ ml) {
+                                                             float* __restrict__ opart, float* __restrict__ ml, int ostg = 0) {
     typedef typename Frag<T>::type FT;
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     constexpr int D = NW * CT * 32, H = D / 64, NQ = (2 * H + 15) / 16;
@@ -363,7 +363,31 @@ __global__ void __launch_bounds__(NW * 64) xattn_step_kernel(const T* __restrict
     // partial O (unnormalised) [i][sp][h][c], m and l [i][sp][h][2] (write-through stores of the
     // partials measured no faster, not kept)
     const int h = lane & 31;
-    if (h < H) {
+    if (ostg) {
+        // (round 6) the wave's O^T tile [H][CT x 32 columns] staged in the free E stages (rows padded by 4 floats),
+        // then written as 16-byte chunks of consecutive columns per lane: every store instruction covers whole
+        // 128-byte lines of the head rows (the direct form below writes 32 bytes of each of 32 rows). Same values.
+        constexpr int OW = CT * 32 + 4;
+        static_assert(NW * H * OW * 4 <= STG_B, "O staging fits the E stages");
+        __syncthreads();  // every wave is done with the last E stage
+        float* so = (float*)lds + wave * H * OW;
+        if (h < H) {
+#pragma unroll
+            for (int k = 0; k < CT; k++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int c = k * 32 + 8 * g + 4 * hh;
+                    *(f32x4*)(so + h * OW + c) = (f32x4){oacc[k][4 * g], oacc[k][4 * g + 1], oacc[k][4 * g + 2], oacc[k][4 * g + 3]};
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        float* ob = opart + ((long)i * splits + sp) * H * D + cw;
+        for (int e = lane; e < H * CT * 8; e += 64) {
+            const int hr = e / (CT * 8), ch = e - hr * (CT * 8);
+            *(f32x4*)(ob + (long)hr * D + ch * 4) = *(const f32x4*)(so + hr * OW + ch * 4);
+        }
+    } else if (h < H) {
         float* o = opart + (((long)i * splits + sp) * H + h) * D;
 #pragma unroll
         for (int k = 0; k < CT; k++)
@@ -580,8 +604,11 @@ static void launch_step_t(const void* enc, const int* slot, const void* qx, int 
     dim3 grid(splits, n);
     // E is streamed once per launch (491 MB at batch 128: more than the MALL holds), so its LDS-DMA
     // loads are non-temporal (aux = 2): 86.6 vs 102.4 us per decode launch, 3075 vs 2921 audio-s/s.
+    // partial-O stores staged through LDS (whole 128-byte lines per instruction): 87.4 -> 85.7 us per 128-clip launch,
+    // the same bits (profiles/r06_xstep_ostg_ab.txt); WHISPER_MI355X_XSTEP_OSTG=0 for the direct stores
+    static const int ostg = getenv("WHISPER_MI355X_XSTEP_OSTG") ? atoi(getenv("WHISPER_MI355X_XSTEP_OSTG")) : 1;
 #define WM_XSTEP(NW_, CT_) \
-    xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml)
+    xattn_step_kernel<T, NW_, CT_, 2><<<grid, NW_ * 64, 0, st>>>((const T*)enc, slot, (const T*)qx, Tn, splits, thr, opart, ml, ostg)
     switch (d) {
         case 384: WM_XSTEP(4, 3); break;
         case 512: WM_XSTEP(8, 2); break;
